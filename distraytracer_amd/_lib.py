@@ -1,0 +1,151 @@
+"""ctypes binding of libdt.so (include/dt.h).
+
+The struct layouts below mirror include/dt.h field by field. Loading fails loudly: there is
+no CPU fallback anywhere in this package — a missing or stale libdt.so is an error, never
+a silent switch to another implementation.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdt.so")
+REPO_ROOT = os.path.dirname(_HERE)
+DATA_DIR = os.path.join(REPO_ROOT, "data")
+
+c_int32, c_uint32, c_int64, c_uint64 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64, ctypes.c_uint64
+c_float, c_double = ctypes.c_float, ctypes.c_double
+D3 = c_double * 3
+
+DT_OK = 0
+DT_OUT_IMAGE = 0
+DT_OUT_SLAB = 1
+
+SHAPE_TYPES = {1: "sphere", 2: "cylinder", 3: "triangle", 4: "rectangle", 5: "rectprism_v2",
+               6: "checkerboard", 7: "checkerboard_hole", 8: "checker_cylinder"}
+
+
+class ShapeDesc(ctypes.Structure):
+    _fields_ = [("type", c_int32), ("model", c_int32), ("material", c_int32), ("emit", c_int32),
+                ("flags", c_uint32), ("tex_frame", c_int32), ("roughness", c_float), ("radius", c_float),
+                ("S", c_float), ("borderwidth", c_float), ("length", c_float), ("width", c_float),
+                ("refr", c_double * 2), ("color", D3), ("color1", D3), ("color2", D3),
+                ("bordercolor", D3), ("center", D3), ("v", D3 * 8), ("mesh_normal", D3),
+                ("uv", (c_double * 2) * 3)]
+
+
+class LightDesc(ctypes.Structure):
+    _fields_ = [("type", c_int32), ("shape_index", c_int32), ("radius", c_float), ("_pad", c_float),
+                ("center", D3), ("color", D3), ("baxis", D3), ("A", D3), ("B", D3), ("D", D3)]
+
+
+class TextureDesc(ctypes.Structure):
+    _fields_ = [("width", c_int32), ("height", c_int32), ("channels", c_int32), ("_pad", c_int32),
+                ("pixels", ctypes.POINTER(ctypes.c_uint8))]
+
+
+class SceneDesc(ctypes.Structure):
+    _fields_ = [("n_shapes", c_int32), ("n_lights", c_int32), ("n_textures", c_int32), ("_pad", c_int32),
+                ("shapes", ctypes.POINTER(ShapeDesc)), ("lights", ctypes.POINTER(LightDesc)),
+                ("textures", ctypes.POINTER(TextureDesc))]
+
+
+class Globals(ctypes.Structure):
+    """render_final_project.cpp:48-137, 1:1 (dt_globals)."""
+    _fields_ = [("xRes", c_int32), ("yRes", c_int32), ("eye", D3), ("lookingAt", D3), ("up", D3),
+                ("aspect", c_float), ("near_plane", c_float), ("fov", c_float), ("aperture", c_float),
+                ("focal_length", c_float), ("use_model", c_int32), ("nogloss", c_int32),
+                ("refr_air", c_float), ("refr_glass", c_float), ("max_depth", c_int32), ("phong", c_float),
+                ("default_col", D3), ("c_isect", c_float), ("c_trav", c_float),
+                ("antialias_samples", c_int32), ("brdf_samples", c_int32), ("blur_samples", c_int32),
+                ("frame_range", c_int32), ("frame_prism", c_int32), ("frame_cloud", c_int32),
+                ("frame_blur", c_int32), ("frame_start", c_int32), ("frame_move1", c_int32),
+                ("frame_move2", c_int32), ("frame_sculp", c_int32), ("total", c_int32),
+                ("far_dist", c_float), ("move_per_frame", c_float), ("tot_move", c_float), ("accel_t", c_float),
+                ("cap_center", D3), ("sundir", D3), ("perlin_cloud", c_int32), ("saturation", c_float),
+                ("clouddist", c_float), ("cloudhoff", c_float), ("sun_outer", D3), ("sun_inner", D3),
+                ("sun_core", D3), ("bluesky", D3), ("redsky", D3), ("reflect", c_int32), ("seed", c_uint32)]
+
+    def copy(self):
+        g = Globals()
+        ctypes.pointer(g)[0] = self
+        return g
+
+
+class Tiles(ctypes.Structure):
+    _fields_ = [("x0", c_int32), ("y0", c_int32), ("x1", c_int32), ("y1", c_int32), ("tile_w", c_int32),
+                ("tile_h", c_int32), ("rank", c_int32), ("world", c_int32), ("layout", c_int32),
+                ("_pad", c_int32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("pixels", c_uint64), ("samples", c_uint64), ("rays", c_uint64), ("shadow_rays", c_uint64),
+                ("sky_pixels", c_uint64), ("uv_out_of_range", c_uint64), ("glossy_exhausted", c_uint64),
+                ("spherelight_exhausted", c_uint64), ("prism_norm_fallback", c_uint64),
+                ("reflect_errors", c_uint64), ("nan_pixels", c_uint64), ("kernel_ms", c_double),
+                ("trace_kernel_ms", c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class BVHNode(ctypes.Structure):
+    _fields_ = [("first_child", c_int32), ("n_children", c_int32), ("first_index", c_int32),
+                ("n_indices", c_int32), ("leaf", c_int32), ("depth", c_int32), ("lbound", D3), ("ubound", D3)]
+
+
+# every symbol include/dt.h declares (checked by tests/test_abi.py)
+EXPORTS = ["dt_abi_version", "dt_last_error", "dt_globals_default", "dt_scene_create", "dt_scene_destroy",
+           "dt_scene_bvh", "dt_slab_floats", "dt_slab_floats_max", "dt_render", "dt_render_async",
+           "dt_collect_stats", "dt_render_sky", "dt_unpack_slabs", "dt_build_scene", "dt_scene_desc_free",
+           "dt_write_ppm", "dt_mocap_bone_table"]
+
+
+class DTError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise DTError("libdt.so not built (%s): run __graft_entry__.build() / make -C "
+                      "distraytracer_amd/csrc" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    sig = {
+        "dt_abi_version": (c_int32, []),
+        "dt_last_error": (ctypes.c_char_p, []),
+        "dt_globals_default": (None, [P(Globals)]),
+        "dt_scene_create": (c_int32, [P(SceneDesc), P(Globals), P(ctypes.c_void_p)]),
+        "dt_scene_destroy": (None, [ctypes.c_void_p]),
+        "dt_scene_bvh": (c_int32, [ctypes.c_void_p, P(BVHNode), c_int32, P(c_int32), c_int32, P(c_int32),
+                                   P(c_int32)]),
+        "dt_slab_floats": (c_int64, [P(Globals), P(Tiles)]),
+        "dt_slab_floats_max": (c_int64, [P(Globals), P(Tiles)]),
+        "dt_render": (c_int32, [ctypes.c_void_p, P(Globals), c_int32, P(Tiles), ctypes.c_void_p, c_int32,
+                                ctypes.c_void_p, P(Stats)]),
+        "dt_render_async": (c_int32, [ctypes.c_void_p, P(Globals), c_int32, P(Tiles), ctypes.c_void_p,
+                                      ctypes.c_void_p]),
+        "dt_collect_stats": (c_int32, [ctypes.c_void_p, ctypes.c_void_p, P(Stats)]),
+        "dt_render_sky": (c_int32, [P(Globals), c_float, P(Tiles), ctypes.c_void_p, c_int32, ctypes.c_void_p,
+                                    P(Stats)]),
+        "dt_unpack_slabs": (c_int32, [P(Globals), P(Tiles), c_int32, ctypes.c_void_p, ctypes.c_void_p, c_int32,
+                                      ctypes.c_void_p]),
+        "dt_build_scene": (c_int32, [ctypes.c_char_p, c_float, P(Globals), ctypes.c_char_p, P(P(SceneDesc))]),
+        "dt_scene_desc_free": (None, [P(SceneDesc)]),
+        "dt_write_ppm": (c_int32, [ctypes.c_char_p, c_int32, c_int32, ctypes.c_void_p]),
+        "dt_mocap_bone_table": (c_int32, [ctypes.c_char_p, ctypes.c_char_p, P(c_int32), c_int32,
+                                          P(c_double), P(c_int32), P(c_int32)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc, what=""):
+    if rc != DT_OK:
+        raise DTError("%s failed (%d): %s" % (what, rc, lib.dt_last_error().decode(errors="replace")))
+    return rc

@@ -1,0 +1,507 @@
+// dt_api.cpp — the C-ABI entry points (include/dt.h) over the HIP kernels.
+// No exception and no exit() crosses the boundary: every entry point returns a status
+// code and leaves a message for dt_last_error().
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "host_internal.h"
+
+using namespace dth;
+
+extern "C" size_t dt_launch_size(void);
+extern "C" size_t dt_scene_struct_offset(void);
+extern "C" size_t dt_params_struct_offset(void);
+extern "C" hipError_t dt_launch_trace(const void* dev_launch, float* out, int grid, hipStream_t stream);
+extern "C" hipError_t dt_launch_sky(const void* dev_launch, float* out, int64_t n_threads, hipStream_t stream);
+extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_t slab_floats, const float* slabs,
+                                       float* image, hipStream_t stream);
+extern "C" const void* dt_trace_kernel_ptr(void);
+
+namespace {
+
+thread_local std::string g_err;
+
+// must match the device-side DScene (dt_kernels.hip)
+struct HScene {
+  const void* nodes;
+  const int32_t* leaf_idx;
+  const void* hdr;
+  const double* geom;
+  const void* mat;
+  const void* lights;
+  const uint8_t* tex;
+  const float* cloud_z;
+  unsigned long long* stats;
+  unsigned long long* queue;
+};
+
+enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
+       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_N = 16 };
+
+int fail(int code, const std::string& msg)
+{
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return fail(DT_E_NO_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));  \
+  } while (0)
+
+template <class T>
+int upload(const std::vector<T>& v, void** dptr)
+{
+  size_t bytes = v.size() * sizeof(T);
+  if (bytes == 0) bytes = 16;
+  HIPCHK(hipMalloc(dptr, bytes));
+  if (!v.empty()) HIPCHK(hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return DT_OK;
+}
+
+int max_resident_waves(const void* kernel_fn, int block)
+{
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 1024;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 1024;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_fn, block, 0) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  return per_cu * prop.multiProcessorCount;
+}
+
+}  // namespace
+
+namespace dth {
+void set_error(const std::string& e) { g_err = e; }
+}  // namespace dth
+
+struct dt_scene {
+  int device = 0;
+  FlatScene flat;
+  void* d_nodes = nullptr;
+  void* d_leaf = nullptr;
+  void* d_hdr = nullptr;
+  void* d_geom = nullptr;
+  void* d_mat = nullptr;
+  void* d_lights = nullptr;
+  void* d_tex = nullptr;
+  void* d_zs = nullptr;
+  size_t zs_cap = 0;
+  unsigned long long* d_stats = nullptr;   // ST_N counters + queue word
+  void* d_launch = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  dtd::DParams last;
+};
+
+extern "C" {
+
+int dt_abi_version(void) { return DT_ABI_VERSION; }
+const char* dt_last_error(void) { return g_err.c_str(); }
+
+void dt_globals_default(dt_globals* g)
+{
+  // render_final_project.cpp:48-138
+  memset(g, 0, sizeof(*g));
+  g->xRes = 1920;
+  g->yRes = 1080;
+  g->eye[0] = -6; g->eye[1] = 0.5; g->eye[2] = 1;
+  g->lookingAt[0] = 0.5; g->lookingAt[1] = 0.5; g->lookingAt[2] = 1;
+  g->up[0] = 0; g->up[1] = 1; g->up[2] = 0;
+  g->aspect = (float)1920 / (float)1080;
+  g->near_plane = 1;
+  g->fov = 45.0f;
+  g->aperture = 0.2f;
+  g->focal_length = 10;
+  g->use_model = 1;
+  g->nogloss = 0;
+  g->refr_air = 1;
+  g->refr_glass = 1.5f;
+  g->max_depth = 10;
+  g->phong = 10;
+  g->c_isect = 1;
+  g->c_trav = 0.33f;
+  g->antialias_samples = 10;
+  g->brdf_samples = 2;
+  g->blur_samples = 2;
+  g->frame_range = 1;
+  g->frame_prism = 960;
+  g->frame_cloud = 1952;
+  g->frame_blur = 1600;
+  g->frame_start = 120;
+  g->frame_move1 = 480;
+  g->frame_move2 = 960;
+  g->frame_sculp = 600;
+  g->total = 2400;
+  g->far_dist = 200;
+  g->move_per_frame = (float)(0.1 / 8);
+  g->tot_move = 0;
+  g->accel_t = (float)(80 / pow(360, 3));
+  g->sundir[0] = 0; g->sundir[1] = 0.1; g->sundir[2] = -1;
+  g->perlin_cloud = 0;
+  g->saturation = 0.2f;
+  g->clouddist = 10;
+  g->cloudhoff = 0.2f;
+  g->sun_outer[0] = 0.9; g->sun_outer[1] = 0.3; g->sun_outer[2] = 0.9;
+  g->sun_inner[0] = 1.0; g->sun_inner[1] = 0.7; g->sun_inner[2] = 0.7;
+  g->sun_core[0] = 1; g->sun_core[1] = 1; g->sun_core[2] = 1;
+  g->bluesky[0] = 0.3; g->bluesky[1] = 0.55; g->bluesky[2] = 0.8;
+  g->redsky[0] = 0.8; g->redsky[1] = 0.8; g->redsky[2] = 0.6;
+  g->reflect = 1;
+  g->seed = 0;
+}
+
+int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** out)
+{
+  if (!desc || !g || !out) return fail(DT_E_INVALID, "null argument");
+  *out = nullptr;
+  dt_scene* s = new dt_scene();
+  std::string err;
+  int rc = flatten_scene(*desc, *g, s->flat, err);
+  if (rc) {
+    delete s;
+    return fail(rc, err);
+  }
+  if (hipGetDevice(&s->device) != hipSuccess) {
+    delete s;
+    return fail(DT_E_NO_DEVICE, "no HIP device");
+  }
+  const FlatScene& f = s->flat;
+  std::vector<int32_t> leaf = f.bvh.leaf_idx;
+  if (leaf.empty()) leaf.push_back(0);
+  if ((rc = upload(f.bvh.nodes, &s->d_nodes)) || (rc = upload(leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
+      (rc = upload(f.geom, &s->d_geom)) || (rc = upload(f.mat, &s->d_mat)) || (rc = upload(f.lights, &s->d_lights)) ||
+      (rc = upload(f.tex, &s->d_tex))) {
+    dt_scene_destroy(s);
+    return rc;
+  }
+  if (hipMalloc((void**)&s->d_stats, sizeof(unsigned long long) * (ST_N + 16)) != hipSuccess ||
+      hipMalloc(&s->d_launch, dt_launch_size()) != hipSuccess || hipEventCreate(&s->ev0) != hipSuccess ||
+      hipEventCreate(&s->ev1) != hipSuccess) {
+    dt_scene_destroy(s);
+    return fail(DT_E_NO_DEVICE, "device allocation failed");
+  }
+  *out = s;
+  return DT_OK;
+}
+
+void dt_scene_destroy(dt_scene* s)
+{
+  if (!s) return;
+  void* bufs[] = {s->d_nodes, s->d_leaf, s->d_hdr, s->d_geom, s->d_mat, s->d_lights, s->d_tex, s->d_zs,
+                  s->d_stats, s->d_launch};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (s->ev0) (void)hipEventDestroy(s->ev0);
+  if (s->ev1) (void)hipEventDestroy(s->ev1);
+  delete s;
+}
+
+int dt_scene_bvh(const dt_scene* s, dt_bvh_node* nodes, int32_t cap, int32_t* indices, int32_t index_cap,
+                 int32_t* n_nodes, int32_t* n_indices)
+{
+  if (!s) return fail(DT_E_INVALID, "null scene");
+  const FlatBVH& b = s->flat.bvh;
+  for (size_t i = 0; i < b.nodes.size() && (int32_t)i < cap; ++i) {
+    const dtd::DNode& n = b.nodes[i];
+    dt_bvh_node& o = nodes[i];
+    o.leaf = b.n_children[i] == 0 ? 1 : 0;
+    o.n_children = b.n_children[i];
+    o.first_child = b.n_children[i] ? (int32_t)i + 1 : -1;
+    o.depth = b.depth[i];
+    o.first_index = o.leaf ? n.first : -1;
+    o.n_indices = o.leaf ? n.count : 0;
+    for (int k = 0; k < 3; ++k) {
+      o.lbound[k] = n.lb[k];
+      o.ubound[k] = n.ub[k];
+    }
+  }
+  for (size_t i = 0; i < b.leaf_idx.size() && (int32_t)i < index_cap; ++i) indices[i] = b.leaf_idx[i];
+  if (n_nodes) *n_nodes = (int32_t)b.nodes.size();
+  if (n_indices) *n_indices = (int32_t)b.leaf_idx.size();
+  return DT_OK;
+}
+
+int64_t dt_slab_floats(const dt_globals* g, const dt_tiles* tiles)
+{
+  dtd::DParams P;
+  std::string err;
+  if (!g || fill_sky_params(*g, 0.0f, tiles, P, err)) return -1;
+  return P.n_owned_tiles * P.tw * P.th * 3;
+}
+
+int64_t dt_slab_floats_max(const dt_globals* g, const dt_tiles* tiles)
+{
+  if (!g || !tiles) return -1;
+  dt_tiles t = *tiles;
+  t.rank = 0;   // rank 0 owns the most tiles
+  return dt_slab_floats(g, &t);
+}
+
+static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame, const dt_tiles* tiles,
+                          dtd::DParams& P, std::vector<float>& zs)
+{
+  std::string err;
+  int rc = fill_params(*g, frame, tiles, P, err);
+  if (rc) return fail(rc, err);
+  const int need = g->max_depth * (2 + (g->brdf_samples > 1 ? g->brdf_samples : 1));
+  if (need > 48) return fail(DT_E_LIMIT, "max_depth*(2+brdf_samples) exceeds the device DFS stack (48)");
+  zs = cloud_z_steps(*g);
+  if (g->perlin_cloud && zs.size() > 2048) return fail(DT_E_LIMIT, "clouddist/0.05 exceeds 2048 march steps");
+  P.n_nodes = (int32_t)sc->flat.bvh.nodes.size();
+  P.n_lights = (int32_t)sc->flat.lights.size();
+  P.n_shapes = (int32_t)sc->flat.hdr.size();
+  return DT_OK;
+}
+
+static int enqueue_render(dt_scene* sc, const dtd::DParams& P, const std::vector<float>& zs, float* out_dev,
+                          hipStream_t st)
+{
+  if (zs.size() > sc->zs_cap) {
+    if (sc->d_zs) (void)hipFree(sc->d_zs);
+    sc->d_zs = nullptr;
+    sc->zs_cap = zs.size() + 64;
+    HIPCHK(hipMalloc(&sc->d_zs, sc->zs_cap * sizeof(float)));
+  }
+  if (!zs.empty()) HIPCHK(hipMemcpyAsync(sc->d_zs, zs.data(), zs.size() * sizeof(float), hipMemcpyHostToDevice, st));
+  std::vector<uint8_t> L(dt_launch_size(), 0);
+  HScene hs;
+  hs.nodes = sc->d_nodes;
+  hs.leaf_idx = (const int32_t*)sc->d_leaf;
+  hs.hdr = sc->d_hdr;
+  hs.geom = (const double*)sc->d_geom;
+  hs.mat = sc->d_mat;
+  hs.lights = sc->d_lights;
+  hs.tex = (const uint8_t*)sc->d_tex;
+  hs.cloud_z = (const float*)sc->d_zs;
+  hs.stats = sc->d_stats;
+  hs.queue = sc->d_stats + ST_N;
+  memcpy(L.data() + dt_scene_struct_offset(), &hs, sizeof(hs));
+  memcpy(L.data() + dt_params_struct_offset(), &P, sizeof(P));
+  HIPCHK(hipMemcpyAsync(sc->d_launch, L.data(), L.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 16), st));
+  static int resident = 0;
+  if (!resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
+  int64_t grid = P.n_items < resident ? P.n_items : resident;
+  if (grid < 1) grid = 1;
+  HIPCHK(hipEventRecord(sc->ev0, st));
+  HIPCHK(dt_launch_trace(sc->d_launch, out_dev, (int)grid, st));
+  HIPCHK(hipEventRecord(sc->ev1, st));
+  sc->timed = true;
+  sc->last = P;
+  // keep the host staging alive until the copy is done
+  HIPCHK(hipStreamSynchronize(st));
+  return DT_OK;
+}
+
+int dt_collect_stats(const dt_scene* sc_c, void* stream, dt_stats* stats)
+{
+  dt_scene* sc = const_cast<dt_scene*>(sc_c);
+  if (!sc) return fail(DT_E_INVALID, "null scene");
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipStreamSynchronize(st));
+  if (!stats) return DT_OK;
+  unsigned long long h[ST_N];
+  HIPCHK(hipMemcpy(h, sc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  memset(stats, 0, sizeof(*stats));
+  const dtd::DParams& P = sc->last;
+  int64_t px = 0;
+  {
+    // pixels rendered = owned pixels inside the window
+    int64_t tiles_y = (P.y1 - P.y0 + P.th - 1) / P.th;
+    for (int64_t k = 0; k < P.n_owned_tiles; ++k) {
+      int64_t t = P.rank + k * P.world;
+      int ty = (int)(t / P.tiles_x), tx = (int)(t % P.tiles_x);
+      (void)tiles_y;
+      int w = P.x1 - (P.x0 + tx * P.tw);
+      int hh = P.y1 - (P.y0 + ty * P.th);
+      w = w < P.tw ? w : P.tw;
+      hh = hh < P.th ? hh : P.th;
+      px += (int64_t)w * hh;
+    }
+  }
+  stats->pixels = px;
+  stats->samples = (uint64_t)px * P.spp;
+  stats->rays = h[ST_RAYS];
+  stats->shadow_rays = h[ST_SHADOW];
+  stats->sky_pixels = h[ST_SKY];
+  stats->uv_out_of_range = h[ST_UV];
+  stats->glossy_exhausted = h[ST_GLOSSY];
+  stats->spherelight_exhausted = h[ST_SPHL];
+  stats->prism_norm_fallback = h[ST_PRISM];
+  stats->reflect_errors = h[ST_REFL] + h[ST_STACK];
+  stats->nan_pixels = h[ST_NAN];
+  if (sc->timed) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, sc->ev0, sc->ev1) == hipSuccess) {
+      stats->kernel_ms = ms;
+      stats->trace_kernel_ms = ms;
+    }
+  }
+  return DT_OK;
+}
+
+int dt_render_async(const dt_scene* sc_c, const dt_globals* g, int32_t frame, const dt_tiles* tiles,
+                    float* out_device, void* stream)
+{
+  dt_scene* sc = const_cast<dt_scene*>(sc_c);
+  if (!sc || !g || !out_device) return fail(DT_E_INVALID, "null argument");
+  dtd::DParams P;
+  std::vector<float> zs;
+  int rc = prepare_render(sc, g, frame, tiles, P, zs);
+  if (rc) return rc;
+  return enqueue_render(sc, P, zs, out_device, (hipStream_t)stream);
+}
+
+int dt_render(const dt_scene* sc_c, const dt_globals* g, int32_t frame, const dt_tiles* tiles, float* out,
+              int32_t out_on_device, void* stream, dt_stats* stats)
+{
+  dt_scene* sc = const_cast<dt_scene*>(sc_c);
+  if (!sc || !g || !out) return fail(DT_E_INVALID, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  dtd::DParams P;
+  std::vector<float> zs;
+  int rc = prepare_render(sc, g, frame, tiles, P, zs);
+  if (rc) return rc;
+  float* dout = out;
+  size_t n_out = P.layout == DT_OUT_SLAB ? (size_t)(P.n_owned_tiles * P.tw * P.th * 3)
+                                         : (size_t)g->xRes * g->yRes * 3;
+  if (!out_on_device) {
+    HIPCHK(hipMalloc((void**)&dout, n_out * sizeof(float)));
+    HIPCHK(hipMemcpyAsync(dout, out, n_out * sizeof(float), hipMemcpyHostToDevice, st));
+  }
+  rc = enqueue_render(sc, P, zs, dout, st);
+  if (rc == DT_OK && !out_on_device) {
+    hipError_t e = hipMemcpyAsync(out, dout, n_out * sizeof(float), hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) rc = fail(DT_E_NO_DEVICE, hipGetErrorString(e));
+  }
+  if (rc == DT_OK) rc = dt_collect_stats(sc, stream, stats);
+  if (!out_on_device) (void)hipFree(dout);
+  return rc;
+}
+
+int dt_render_sky(const dt_globals* g, float frame, const dt_tiles* tiles, float* out, int32_t out_on_device,
+                  void* stream, dt_stats* stats)
+{
+  if (!g || !out) return fail(DT_E_INVALID, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  dtd::DParams P;
+  std::string err;
+  int rc = fill_sky_params(*g, frame, tiles, P, err);
+  if (rc) return fail(rc, err);
+  std::vector<float> zs = cloud_z_steps(*g);
+  void *d_zs = nullptr, *d_launch = nullptr;
+  float* dout = out;
+  size_t n_out = P.layout == DT_OUT_SLAB ? (size_t)(P.n_owned_tiles * P.tw * P.th * 3) : (size_t)g->xRes * g->yRes * 3;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  std::vector<uint8_t> L(dt_launch_size(), 0);
+  HScene hs;
+  memset(&hs, 0, sizeof(hs));
+  HIPCHK(hipMalloc(&d_zs, (zs.size() + 1) * sizeof(float)));
+  HIPCHK(hipMalloc(&d_launch, L.size()));
+  HIPCHK(hipMemcpyAsync(d_zs, zs.data(), zs.size() * sizeof(float), hipMemcpyHostToDevice, st));
+  hs.cloud_z = (const float*)d_zs;
+  memcpy(L.data() + dt_scene_struct_offset(), &hs, sizeof(hs));
+  memcpy(L.data() + dt_params_struct_offset(), &P, sizeof(P));
+  HIPCHK(hipMemcpyAsync(d_launch, L.data(), L.size(), hipMemcpyHostToDevice, st));
+  if (!out_on_device) {
+    HIPCHK(hipMalloc((void**)&dout, n_out * sizeof(float)));
+    HIPCHK(hipMemcpyAsync(dout, out, n_out * sizeof(float), hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipEventRecord(e0, st));
+  HIPCHK(dt_launch_sky(d_launch, dout, P.n_owned_tiles * P.tw * P.th, st));
+  HIPCHK(hipEventRecord(e1, st));
+  if (!out_on_device) HIPCHK(hipMemcpyAsync(out, dout, n_out * sizeof(float), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (stats) {
+    memset(stats, 0, sizeof(*stats));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    stats->kernel_ms = ms;
+    stats->trace_kernel_ms = ms;
+    int64_t w = P.x1 - P.x0, h = P.y1 - P.y0;
+    stats->pixels = P.world == 1 ? (uint64_t)(w * h) : 0;
+    stats->samples = stats->pixels;
+    stats->sky_pixels = stats->pixels;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(d_zs);
+  (void)hipFree(d_launch);
+  if (!out_on_device) (void)hipFree(dout);
+  return DT_OK;
+}
+
+int dt_unpack_slabs(const dt_globals* g, const dt_tiles* tiles, int32_t world, const float* slabs, float* image,
+                    int32_t on_device, void* stream)
+{
+  if (!g || !tiles || !slabs || !image || world < 1) return fail(DT_E_INVALID, "null argument");
+  dt_tiles t = *tiles;
+  t.rank = 0;
+  t.world = world;
+  dtd::DParams P;
+  std::string err;
+  int rc = fill_sky_params(*g, 0.0f, &t, P, err);
+  if (rc) return fail(rc, err);
+  int64_t slab_floats = P.n_owned_tiles * P.tw * P.th * 3;
+  if (!on_device) {
+    // host scatter
+    int64_t ntiles = (int64_t)P.tiles_x * ((P.y1 - P.y0 + P.th - 1) / P.th);
+    for (int r = 0; r < world; ++r) {
+      int64_t owned = ntiles > r ? (ntiles - r + world - 1) / world : 0;
+      for (int64_t slot = 0; slot < owned; ++slot) {
+        int64_t tid = r + slot * world;
+        int ty = (int)(tid / P.tiles_x), tx = (int)(tid % P.tiles_x);
+        for (int py = 0; py < P.th; ++py)
+          for (int px = 0; px < P.tw; ++px) {
+            int x = P.x0 + tx * P.tw + px, y = P.y0 + ty * P.th + py;
+            if (x >= P.x1 || y >= P.y1) continue;
+            const float* s = slabs + r * slab_floats + ((slot * P.th + py) * P.tw + px) * 3;
+            float* d = image + 3 * ((int64_t)(g->yRes - 1 - y) * g->xRes + x);
+            d[0] = s[0];
+            d[1] = s[1];
+            d[2] = s[2];
+          }
+      }
+    }
+    return DT_OK;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  void* d_launch = nullptr;
+  std::vector<uint8_t> L(dt_launch_size(), 0);
+  memcpy(L.data() + dt_params_struct_offset(), &P, sizeof(P));
+  HIPCHK(hipMalloc(&d_launch, L.size()));
+  HIPCHK(hipMemcpyAsync(d_launch, L.data(), L.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(dt_launch_unpack(d_launch, world, slab_floats, slabs, image, st));
+  HIPCHK(hipStreamSynchronize(st));
+  (void)hipFree(d_launch);
+  return DT_OK;
+}
+
+int dt_write_ppm(const char* filename, int32_t xRes, int32_t yRes, const float* values)
+{
+  // helpers.h:174-195: float -> unsigned char conversion (truncation)
+  if (!filename || !values || xRes <= 0 || yRes <= 0) return fail(DT_E_INVALID, "bad arguments");
+  size_t total = (size_t)xRes * yRes * 3;
+  std::vector<unsigned char> px(total);
+  for (size_t i = 0; i < total; ++i) px[i] = (unsigned char)values[i];
+  FILE* fp = fopen(filename, "wb");
+  if (!fp) return fail(DT_E_IO, std::string("could not open ") + filename);
+  fprintf(fp, "P6\n%d %d\n255\n", xRes, yRes);
+  fwrite(px.data(), 1, total, fp);
+  fclose(fp);
+  return DT_OK;
+}
+
+}  // extern "C"

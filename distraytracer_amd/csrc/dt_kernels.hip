@@ -1,0 +1,1458 @@
+// dt_kernels.hip — gfx950 (CDNA4) kernels for the distraytracer per-pixel render loop.
+//
+// Reference hot path: renderImage pixel/sample loop (render_final_project.cpp:1031-1218),
+// rayColor (487-961), cloudColor/skyColor (146-192), noise.h, geometry.cpp primitives.
+// Design:
+//   * one wave64 = the samples of one pixel (spp >= 64: 64 samples per chunk) or of
+//     64/spp pixels: the 64 lanes shoot nearly identical primary rays (same pixel, DoF
+//     jitter only), so BVH traversal, shape dispatch and shading stay wave-coherent;
+//   * BVH traversal is stackless and WAVE-UNIFORM over the reference's static pre-order:
+//     node/shape data are read with uniform indices (scalar loads), each lane keeps one
+//     int "resume" index, a __ballot decides descend/skip. Per-lane visit order equals the
+//     reference's gather order, so closest-hit ties resolve identically;
+//   * rayColor's recursion tree runs as a per-lane DFS on a private stack in pre-order,
+//     with a FINISH entry per node so each node's own light is added after its children,
+//     exactly as the reference's `color +=` order;
+//   * a persistent grid dequeues pixel groups from an atomic counter;
+//   * sky (cloudColor, 200-step value-noise march) is per-pixel deterministic (Q4): it is
+//     computed once per pixel by all 64 lanes cooperatively, only for pixels with misses.
+// Numerics: FP64 wherever the reference uses VEC3/double, FP32 where it declares float,
+// compiled with -ffp-contract=off (no FMA contraction), correctly rounded div/sqrt.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dt.h"
+#include "dt_math.h"
+#include "dt_scene_dev.h"
+
+using namespace dtm;
+using namespace dtd;
+
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
+#define DT_STACK_MAX 48
+#define DT_MAX_CLOUD_STEPS 2048
+#define DT_WAVE 64
+
+enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
+       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_N = 16 };
+
+__constant__ uint32_t c_primes[10][3] = {
+    {995615039u, 600173719u, 701464987u}, {831731269u, 162318869u, 136250887u},
+    {174329291u, 946737083u, 245679977u}, {362489573u, 795918041u, 350777237u},
+    {457025711u, 880830799u, 909678923u}, {787070341u, 177340217u, 593320781u},
+    {405493717u, 291031019u, 391950901u}, {458904767u, 676625681u, 424452397u},
+    {531736441u, 939683957u, 810651871u}, {997169939u, 842027887u, 423882827u}};
+
+struct DScene {
+  const DNode* nodes;
+  const int32_t* leaf_idx;
+  const DShapeHdr* hdr;
+  const double* geom;
+  const DMat* mat;
+  const DLight* lights;
+  const uint8_t* tex;
+  const float* cloud_z;   // float z sequence of cloudColor's loop (cpp:172)
+  unsigned long long* stats;
+  unsigned long long* queue;
+};
+
+// =====================================================================================
+// value noise (noise.h:25-136) and sky (render_final_project.cpp:146-192)
+// =====================================================================================
+__device__ __forceinline__ double noise3d(int i, int x, int y, int z)
+{
+  // (int)(x + y*57 + z*pow(57,2)) is an exact integer for in-range lattice coordinates
+  int n = x + y * 57 + z * 3249;
+  uint32_t un = (uint32_t)n;
+  un = (un << 13) ^ un;
+  uint32_t t = (un * (un * un * c_primes[i][0] + c_primes[i][1]) + c_primes[i][2]) & 0x7fffffffu;
+  return 1.0 - (double)(int)t / 1073741823.0;
+}
+
+// noise.h:51-70, summation order preserved term by term
+__device__ __forceinline__ double smoothed3d(int i, int x, int y, int z)
+{
+#define N(dx, dy, dz) noise3d(i, x + (dx), y + (dy), z + (dz))
+  double corners = N(-1, -1, -1) + N(1, -1, -1) + N(-1, 1, -1) + N(1, 1, -1) + N(-1, -1, 1) +
+                   N(1, -1, 1) + N(-1, 1, 1) + N(1, 1, 1);
+  double sides = N(-1, 0, 0) + N(1, 0, 0) + N(0, 1, 0) + N(0, -1, 0) + N(0, 0, -1) + N(0, 0, 1);
+  double dgsides = N(-1, 0, -1) + N(1, 0, -1) + N(0, 1, -1) + N(0, -1, -1) + N(-1, 0, 1) +
+                   N(1, 0, 1) + N(0, 1, 1) + N(-1, -1, 0) + N(0, -1, 1) + N(1, -1, 0) +
+                   N(-1, 1, 0) + N(1, 1, 0);
+  double center = N(0, 0, 0);
+#undef N
+  const double alpha = 9.0 / 18, beta = 2.0 / (8 * 18), gamma = 4.0 / (6 * 18),
+               delta = 3.0 / (12 * 18);
+  return alpha * center + beta * corners + gamma * sides + delta * dgsides;
+}
+
+__device__ __forceinline__ double cos_f(double x) { return (1 - cos(x * M_PI)) * 0.5; }
+__device__ __forceinline__ double lerp_f(double a, double b, double f) { return a * (1 - f) + b * f; }
+
+// noise.h:81-107; cos(angle) of the same fractional part is evaluated once (same bits)
+__device__ double interpolated_noise3d(int i, double x, double y, double z)
+{
+  int ix = (int)x, iy = (int)y, iz = (int)z;
+  double fx = x - ix, fy = y - iy, fz = z - iz;
+  double v1 = smoothed3d(i, ix, iy, iz);
+  double v2 = smoothed3d(i, ix + 1, iy, iz);
+  double v3_ = smoothed3d(i, ix, iy + 1, iz);
+  double v4 = smoothed3d(i, ix + 1, iy + 1, iz);
+  double v5 = smoothed3d(i, ix, iy, iz + 1);
+  double v6 = smoothed3d(i, ix + 1, iy, iz + 1);
+  double v7 = smoothed3d(i, ix, iy + 1, iz + 1);
+  double v8 = smoothed3d(i, ix + 1, iy + 1, iz + 1);
+  double cx = cos_f(fx), cy = cos_f(fy), cz = cos_f(fz);
+  double w1 = lerp_f(v5, v6, cx), w2 = lerp_f(v7, v8, cx);
+  double w3 = lerp_f(v1, v2, cx), w4 = lerp_f(v3_, v4, cx);
+  double i1 = lerp_f(w3, w4, cy), i2 = lerp_f(w1, w2, cy);
+  return lerp_f(i1, i2, cz);
+}
+
+// noise.h:124-136 (4 octaves; frequency 8,4,2,1 and amplitude .125,.25,.5,1 are exact)
+__device__ double value_noise3d(double x, double y, double z)
+{
+  double total = 0;
+  double frequency = 16.0, amplitude = 0.0625;
+  for (int i = 0; i < 4; ++i) {
+    frequency /= 2;
+    amplitude /= 0.5;
+    total += interpolated_noise3d(i, x * frequency, y * frequency, z * frequency) * amplitude;
+  }
+  return total;
+}
+
+// render_final_project.cpp:146-162
+__device__ V3 sky_color(const DParams& P, V3 ray)
+{
+  V3 color = v3(0, 0, 0);
+  V3 rnorm = normalized(ray);
+  V3 sun = v3a(P.sun);
+  float sundot = clampf01((float)dot(rnorm, sun));
+  double sd = sundot;
+  double p1 = pow(sd, 1.0), p2 = pow(sd, 2.0), p256 = pow(sd, 256.0);
+  V3 term = add(add(mul(p1, mul(0.05, v3a(P.sun_outer))), mul(p2, mul(0.1, v3a(P.sun_inner)))),
+                mul(p256, mul(0.9, v3a(P.sun_core))));
+  color = add(color, term);
+  double p8 = pow(sd, 8.0);
+  V3 sky = add(mul(1 - 1.5 * p8, v3a(P.bluesky)), mul(p8, mul(1.5, v3a(P.redsky))));
+  color = add(color, mul(1.0 - 0.8 * rnorm.y, sky));
+  return color;
+}
+
+// one march step of cloudColor (cpp:172-185): density, or -1 when the step adds nothing
+__device__ __forceinline__ float cloud_step(const DParams& P, float z, V3 ray)
+{
+  V3 p = add(v3(0, 0, 0), mul(z, ray));
+  float noise = (float)(0.7 * value_noise3d(p.x, p.y, p.z + P.frame_f));
+  float cd = (float)((p.y + noise) + P.cloudhoff);
+  if (cd < 0) return clampf01(fabsf(cd));
+  return -1.0f;
+}
+
+__device__ __forceinline__ double cloud_apply(double c, double skyrev, float density)
+{
+  double cloudcolor = 1 - density * skyrev;
+  return (1 - density * 0.4) * c + density * 0.4 * cloudcolor;
+}
+
+// cpp:187-191 contrast + saturation
+__device__ V3 cloud_finish(const DParams& P, V3 color)
+{
+  color = v3(clampf01((float)color.x), clampf01((float)color.y), clampf01((float)color.z));
+  color = sub(mul(3, v3(pow(color.x, 2.0), pow(color.y, 2.0), pow(color.z, 2.0))),
+              mul(2, v3(pow(color.x, 3.0), pow(color.y, 3.0), pow(color.z, 3.0))));
+  double s = (color.x + color.y) + color.z;
+  V3 grey = v3(0.33 * s, 0.33 * s, 0.33 * s);
+  return sub(mul(1 + P.saturation, color), mul(P.saturation, grey));
+}
+
+// full cloudColor on one lane
+__device__ V3 cloud_color_lane(const DParams& P, const float* __restrict__ zs, V3 ray)
+{
+  V3 sky = sky_color(P, ray);
+  V3 color = sky;
+  for (int s = 0; s < P.n_cloud_steps; ++s) {
+    float d = cloud_step(P, zs[s], ray);
+    if (d >= 0.0f) {
+      color.x = cloud_apply(color.x, sky.z, d);
+      color.y = cloud_apply(color.y, sky.y, d);
+      color.z = cloud_apply(color.z, sky.x, d);
+    }
+  }
+  return cloud_finish(P, color);
+}
+
+// cloudColor for one (wave-uniform) ray computed by all 64 lanes: the march steps are
+// spread over lanes (the noise is 99% of the work), the per-channel recurrence then runs
+// on lanes 0..2 in step order, so every addition happens in the reference's order.
+__device__ V3 cloud_color_coop(const DParams& P, const float* __restrict__ zs, V3 ray,
+                               float* __restrict__ dens, double* __restrict__ chan)
+{
+  const int lane = threadIdx.x & 63;
+  V3 sky = sky_color(P, ray);
+  for (int s = lane; s < P.n_cloud_steps; s += DT_WAVE) dens[s] = cloud_step(P, zs[s], ray);
+  __syncthreads();
+  if (lane < 3) {
+    double c = lane == 0 ? sky.x : (lane == 1 ? sky.y : sky.z);
+    double rev = lane == 0 ? sky.z : (lane == 1 ? sky.y : sky.x);
+    for (int s = 0; s < P.n_cloud_steps; ++s) {
+      float d = dens[s];
+      if (d >= 0.0f) c = cloud_apply(c, rev, d);
+    }
+    chan[lane] = c;
+  }
+  __syncthreads();
+  V3 col = v3(chan[0], chan[1], chan[2]);
+  __syncthreads();
+  return cloud_finish(P, col);
+}
+
+// =====================================================================================
+// counter RNG: Philox4x32-10 (oracle/oracle.c or_philox4x32)
+// =====================================================================================
+__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                       uint32_t k1, uint32_t o[4])
+{
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  o[0] = c0; o[1] = c1; o[2] = c2; o[3] = c3;
+}
+__device__ __forceinline__ double u01(uint32_t w0, uint32_t w1)
+{
+  return ((double)(w0 >> 5) * 67108864.0 + (double)(w1 >> 6)) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ uint32_t fmix32(uint32_t h)
+{
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t root_key(int pass) { return fmix32(0x12345678u + (uint32_t)pass); }
+__device__ __forceinline__ uint32_t child_key(uint32_t parent, int slot)
+{
+  return fmix32(parent * 0x9E3779B1u + (uint32_t)slot + 1u);
+}
+enum { P_DOF = 1, P_LIGHT = 2, P_SPHL = 3, P_GLOSSY = 4, P_BLUR = 5 };
+
+struct Rng {
+  uint32_t k0, k1, pixel, sample;
+  __device__ void draw(uint32_t node, uint32_t purpose, uint32_t sub, double& u0, double& u1) const
+  {
+    uint32_t o[4];
+    philox(pixel, sample, node, (purpose << 24) | sub, k0, k1, o);
+    u0 = u01(o[0], o[1]);
+    u1 = u01(o[2], o[3]);
+  }
+};
+
+// =====================================================================================
+// primitives (geometry.cpp), geometry from the precomputed pool
+// =====================================================================================
+__device__ __forceinline__ V3 G3(const double* __restrict__ g, int o) { return v3(g[o], g[o + 1], g[o + 2]); }
+
+// Rectangle plane + quad bounds test (geometry.cpp:640-741 / 2292-2312): R record
+__device__ __forceinline__ bool rect_hit_R(const double* __restrict__ R, V3 ray, V3 start, float eps,
+                                           float& t_out, float& ch1, float& ch2)
+{
+  V3 A = G3(R, R_A), n = G3(R, R_N);
+  float dn = (float)dot(ray, n);
+  if (dn == 0) return false;
+  float t_final = (float)(dot(sub(A, start), n) / dn);
+  if (t_final <= eps) return false;
+  V3 point = add(start, mul(t_final, ray));
+  V3 V_hit = sub(point, A);
+  float check1 = (float)dot(G3(R, R_V1N), V_hit);
+  float check2 = (float)dot(G3(R, R_V2N), V_hit);
+  if (0 <= check1 && check1 <= R[R_LEN1] && 0 <= check2 && check2 <= R[R_LEN2]) {
+    t_out = t_final;
+    ch1 = check1;
+    ch2 = check2;
+    return true;
+  }
+  return false;
+}
+
+// same, R computed from (shifted) raw vertices — motion-blur retraces of "rectangle" shapes
+__device__ bool rect_hit_raw(V3 A, V3 B, V3 C, V3 D, V3 ray, V3 start, float eps, float& t_out)
+{
+  V3 n = normalized(normalized(cross(sub(B, A), sub(C, A))));
+  float dn = (float)dot(ray, n);
+  if (dn == 0) return false;
+  float t_final = (float)(dot(sub(A, start), n) / dn);
+  if (t_final <= eps) return false;
+  V3 point = add(start, mul(t_final, ray));
+  V3 V_hit = sub(point, A);
+  V3 V1 = sub(B, A), V2 = sub(D, A);
+  float check1 = (float)dot(normalized(V1), V_hit);
+  float check2 = (float)dot(normalized(V2), V_hit);
+  if (0 <= check1 && check1 <= norm(V1) && 0 <= check2 && check2 <= norm(V2)) {
+    t_out = t_final;
+    return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ void shifted_rect(const double* __restrict__ g, float shift, V3& A, V3& B,
+                                             V3& C, V3& D)
+{
+  A = G3(g, RC_A); B = G3(g, RC_B); C = G3(g, RC_C); D = G3(g, RC_D);
+  A.y = A.y + shift; B.y = B.y + shift; C.y = C.y + shift; D.y = D.y + shift;
+}
+
+// quadratic of Sphere/Cylinder (geometry.cpp:108-124 / 246-256)
+__device__ __forceinline__ bool quad_roots(float A, float B, float C, float& t0, float& t1)
+{
+  float disc = (float)(pow((double)B, 2.0) - (double)(4 * A * C));
+  if (disc < 0) return false;
+  float sq = sqrtf(disc);
+  t0 = (-B + sq) / (2 * A);
+  t1 = (-B - sq) / (2 * A);
+  return true;
+}
+
+__device__ __forceinline__ bool sphere_hit(const double* __restrict__ g, V3 ray, V3 start, float& t,
+                                           int& inside)
+{
+  V3 sc = sub(start, G3(g, SP_C));
+  float A = (float)dot(ray, ray);
+  float B = (float)(2 * dot(ray, sc));
+  float C = (float)(dot(sc, sc) - g[SP_R2]);
+  float t0, t1;
+  if (!quad_roots(A, B, C, t0, t1)) return false;
+  if (t0 <= 0.001 && t1 <= 0.001) { inside = 0; return false; }
+  if (t0 <= 0.001 || t1 <= 0.001) { t = fmaxr(t0, t1); inside = 1; return true; }
+  t = fminr(t0, t1);
+  inside = 0;
+  return true;
+}
+
+__device__ __forceinline__ bool sphere_shadow(const double* __restrict__ g, V3 ray, V3 start, float t_max)
+{
+  const float eps = 1e-3f;
+  V3 sc = sub(start, G3(g, SP_C));
+  float A = (float)dot(ray, ray);
+  float B = (float)(2 * dot(ray, sc));
+  float C = (float)(dot(sc, sc) - g[SP_R2]);
+  float t0, t1;
+  if (!quad_roots(A, B, C, t0, t1)) return false;
+  return !((t0 <= eps || t0 >= t_max) && (t1 <= eps || t1 >= t_max));
+}
+
+__device__ __forceinline__ void cyl_coef(const double* __restrict__ g, V3 ray, V3 start, float& A,
+                                         float& B, float& C)
+{
+  V3 axis = G3(g, CY_AX);
+  V3 rap = sub(ray, mul(dot(ray, axis), axis));
+  V3 sc1 = sub(start, G3(g, CY_C1));
+  V3 cst = sub(sc1, mul(dot(sc1, axis), axis));
+  A = (float)dot(rap, rap);
+  B = (float)(2 * dot(rap, cst));
+  C = (float)(dot(cst, cst) - g[CY_R2]);
+}
+
+__device__ __forceinline__ bool cyl_in_caps(const double* __restrict__ g, V3 p)
+{
+  V3 axis = G3(g, CY_AX);
+  return dot(axis, sub(p, G3(g, CY_C1))) > 0 && dot(axis, sub(p, G3(g, CY_C2))) < 0;
+}
+
+__device__ bool cyl_hit(const double* __restrict__ g, V3 ray, V3 start, float& t, int& inside)
+{
+  const float eps = 1e-3f;
+  float A, B, C, t1, t2;
+  cyl_coef(g, ray, start, A, B, C);
+  if (!quad_roots(A, B, C, t1, t2)) return false;
+  if (t1 <= eps && t2 <= eps) { inside = 0; return false; }
+  if (t1 <= eps || t2 <= eps) {
+    if (cyl_in_caps(g, add(start, mul(t1, ray)))) { t = t1; inside = 1; return true; }
+    return false;
+  }
+  if (cyl_in_caps(g, add(start, mul(t2, ray)))) { t = t2; inside = 0; return true; }
+  return false;
+}
+
+__device__ bool cyl_shadow(const double* __restrict__ g, V3 ray, V3 start, float t_max)
+{
+  const float eps = 1e-3f;
+  float A, B, C, t1, t2;
+  cyl_coef(g, ray, start, A, B, C);
+  if (!quad_roots(A, B, C, t1, t2)) return false;
+  if ((t1 <= eps || t1 >= t_max) && (t2 <= eps || t2 >= t_max)) return false;
+  if (t1 <= eps || t2 <= eps) return cyl_in_caps(g, add(start, mul(t1, ray))) && t1 < t_max;
+  return cyl_in_caps(g, add(start, mul(t2, ray))) && t2 < t_max;
+}
+
+// Moller-Trumbore (geometry.cpp:488-586); returns 0 miss, else writes t_final
+__device__ __forceinline__ bool tri_core(const double* __restrict__ g, V3 ray, V3 start, float& t_final)
+{
+  V3 r1 = G3(g, TR_R1), r2 = G3(g, TR_R2);
+  V3 h = cross(ray, r2);
+  float det = (float)dot(r1, h);
+  float invdet = (float)(1.0 / det);
+  if (det >= -0.0001 && det <= 0.0001) return false;
+  V3 A0 = sub(start, G3(g, TR_A));
+  float u = (float)(invdet * dot(A0, h));
+  if (u < 0 || u > 1) return false;
+  V3 DA0 = cross(A0, r1);
+  float v = (float)(dot(ray, DA0) * invdet);
+  if (v < 0 || u + v > 1) return false;
+  t_final = (float)(dot(r2, DA0) * invdet);
+  return true;
+}
+
+// segmentIntersect (geometry.cpp:44-72) for Checkerboard's edge-on case
+__device__ bool segment_hit(V3 A, V3 B, V3 ray, V3 origin)
+{
+  V3 P3 = add(ray, origin), P4 = origin;
+  V3 d13 = sub(A, P3), d43 = sub(P4, P3), d21 = sub(B, A);
+  float u1 = (float)((dot(d13, d43) * dot(d43, d21) - dot(d13, d21) * dot(d43, d43)) /
+                     (pow(norm(d21), 2.0) * pow(norm(d43), 2.0) - pow(dot(d43, d21), 2.0)));
+  float u2 = (float)((dot(d13, d43) + u1 * dot(d43, d21)) / pow(norm(d43), 2.0));
+  if (u1 < 0 || u1 > 1) return false;
+  if (u2 < 0) return false;
+  V3 p1 = add(A, mul(u1, sub(B, A)));
+  V3 p2 = add(origin, mul(u2, ray));
+  return norm(sub(p2, p1)) < 1e-4;
+}
+
+// GeoPrimitive::intersect. t only written when the reference writes it (Q16).
+__device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, const double* __restrict__ g,
+                          V3 ray, V3 start, float shift, float& t, int& inside, V3& ccol, int& has_ccol)
+{
+  has_ccol = 0;
+  switch (type) {
+    case DT_SHAPE_SPHERE:
+      return sphere_hit(g, ray, start, t, inside);
+    case DT_SHAPE_CYLINDER:
+    case DT_SHAPE_CHECKER_CYLINDER:
+      return cyl_hit(g, ray, start, t, inside);
+    case DT_SHAPE_TRIANGLE: {
+      inside = 0;
+      float tf;
+      if (!tri_core(g, ray, start, tf)) return false;
+      if (tf > 0.0001) {
+        if ((flags & DT_F_MESH) && dot(ray, G3(g, TR_MN)) > 0) inside = 1;
+        t = tf;
+        return true;
+      }
+      return false;
+    }
+    case DT_SHAPE_RECTANGLE: {
+      inside = 0;
+      float tt, c1, c2;
+      if ((flags & DT_F_NAMED_RECT) && shift != 0.0f) {
+        V3 A, B, C, D;
+        shifted_rect(g, shift, A, B, C, D);
+        if (rect_hit_raw(A, B, C, D, ray, start, 1e-4f, tt)) { t = tt; return true; }
+        return false;
+      }
+      if (rect_hit_R(g + RC_R, ray, start, 1e-4f, tt, c1, c2)) { t = tt; return true; }
+      return false;
+    }
+    case DT_SHAPE_RECTPRISM_V2: {
+      float tmin = FLT_MAX, tt, c1, c2;
+#pragma unroll 1
+      for (int f = 0; f < 6; ++f) {
+        if (rect_hit_R(g + PR_F + f * R_SIZE, ray, start, 1e-4f, tt, c1, c2)) {
+          if (tt < tmin) { tmin = tt; inside = 0; }
+        }
+      }
+      if (tmin < FLT_MAX) { t = tmin; return true; }
+      return false;
+    }
+    case DT_SHAPE_CHECKERBOARD:
+    case DT_SHAPE_CHECKERBOARD_HOLE: {
+      inside = 0;
+      if (dot(G3(g, CK_GN), ray) == 0) {
+        V3 A = G3(g, CK_A), B = G3(g, CK_B), C = G3(g, CK_C), D = G3(g, CK_D);
+        // edge-on: returns true without t; colour keeps its construction value
+        if (segment_hit(A, B, ray, start) || segment_hit(A, D, ray, start) ||
+            segment_hit(B, C, ray, start) || segment_hit(C, D, ray, start)) {
+          ccol = G3(g, CK_COL);
+          has_ccol = 1;
+          return true;
+        }
+        return false;
+      }
+      float tt, ch1, ch2;
+      if (!rect_hit_R(g + CK_R, ray, start, 1e-3f, tt, ch1, ch2)) return false;
+      if (type == DT_SHAPE_CHECKERBOARD_HOLE) {
+        float th, a, b;
+        if (rect_hit_R(g + CK_HOLE, ray, start, 1e-4f, th, a, b)) return false;
+      }
+      t = tt;
+      float Sq = (float)g[CK_S];
+      int i = (int)(ch1 / Sq), j = (int)(ch2 / Sq);
+      V3 col = G3(g, CK_COL);
+      if (i % 2 == 0) {
+        if (j % 2 == 0) col = G3(g, CK_COL1);
+        if (j % 2 == 1) col = G3(g, CK_COL2);
+      }
+      if (i % 2 == 1) {
+        if (j % 2 == 0) col = G3(g, CK_COL2);
+        if (j % 2 == 1) col = G3(g, CK_COL1);
+      }
+      ccol = col;
+      has_ccol = 1;
+      return true;
+    }
+  }
+  return false;
+}
+
+// GeoPrimitive::intersectShadow
+__device__ bool shape_shadow(int type, uint32_t flags, const double* __restrict__ g, V3 ray, V3 start,
+                             float t_max, float shift)
+{
+  float tt, a, b;
+  switch (type) {
+    case DT_SHAPE_SPHERE:
+      return sphere_shadow(g, ray, start, t_max);
+    case DT_SHAPE_CYLINDER:
+    case DT_SHAPE_CHECKER_CYLINDER:
+      return cyl_shadow(g, ray, start, t_max);
+    case DT_SHAPE_TRIANGLE: {
+      float tf;
+      if (!tri_core(g, ray, start, tf)) return false;
+      return tf > 0.001 && tf < t_max;
+    }
+    case DT_SHAPE_RECTANGLE:
+      if ((flags & DT_F_NAMED_RECT) && shift != 0.0f) {
+        V3 A, B, C, D;
+        shifted_rect(g, shift, A, B, C, D);
+        return rect_hit_raw(A, B, C, D, ray, start, 1e-4f, tt) && tt < t_max;
+      }
+      return rect_hit_R(g + RC_R, ray, start, 1e-4f, tt, a, b) && tt < t_max;
+    case DT_SHAPE_CHECKERBOARD:
+      return rect_hit_R(g + CK_R, ray, start, 1e-4f, tt, a, b) && tt < t_max;
+    case DT_SHAPE_RECTPRISM_V2:
+#pragma unroll 1
+      for (int f = 0; f < 6; ++f)
+        if (rect_hit_R(g + PR_F + f * R_SIZE, ray, start, 1e-4f, tt, a, b) && tt < t_max) return true;
+      return false;
+    case DT_SHAPE_CHECKERBOARD_HOLE:
+      if (rect_hit_R(g + CK_R, ray, start, 1e-3f, tt, a, b) && tt < t_max) {
+        if (rect_hit_R(g + CK_HOLE, ray, start, 1e-4f, tt, a, b) && tt < t_max) return false;
+        return true;
+      }
+      return false;
+  }
+  return false;
+}
+
+// GeoPrimitive::getNorm (per-lane shape index)
+__device__ V3 shape_norm(int type, uint32_t flags, const double* __restrict__ g, V3 p, float shift,
+                         unsigned long long* st_prism)
+{
+  switch (type) {
+    case DT_SHAPE_SPHERE: {
+      V3 n = sub(p, G3(g, SP_C));
+      return divs(n, norm(n));
+    }
+    case DT_SHAPE_CYLINDER:
+    case DT_SHAPE_CHECKER_CYLINDER: {
+      V3 axis = G3(g, CY_AX);
+      V3 pc = sub(p, G3(g, CY_C1));
+      return normalized(sub(pc, mul(dot(pc, axis), axis)));
+    }
+    case DT_SHAPE_TRIANGLE:
+      return normalized(cross(G3(g, TR_R1), G3(g, TR_R2)));
+    case DT_SHAPE_RECTANGLE: {
+      V3 A, B, C, D;
+      if ((flags & DT_F_NAMED_RECT) && shift != 0.0f) shifted_rect(g, shift, A, B, C, D);
+      else { A = G3(g, RC_A); B = G3(g, RC_B); C = G3(g, RC_C); }
+      return normalized(cross(sub(B, A), sub(C, A)));
+    }
+    case DT_SHAPE_CHECKERBOARD:
+    case DT_SHAPE_CHECKERBOARD_HOLE:
+      return G3(g, CK_GN);
+    case DT_SHAPE_RECTPRISM_V2: {
+      const float eps = 1e-3f;
+      V3 A = G3(g, PR_A), G = G3(g, PR_G);
+      V3 nb = G3(g, PR_NBOT), nr = G3(g, PR_NRIGHT), nf = G3(g, PR_NFRONT);
+      V3 pa = normalized(sub(p, A)), pg = normalized(sub(p, G));
+      float pa_bot = (float)fabs(dot(pa, nb)), pg_bot = (float)fabs(dot(pg, nb));
+      if (pa_bot <= eps || pg_bot <= eps) return nb;
+      float pa_right = (float)fabs(dot(pa, nr)), pg_right = (float)fabs(dot(pg, nr));
+      if (pa_right <= eps || pg_right <= eps) return nr;
+      float pa_front = (float)fabs(dot(pa, nf)), pg_front = (float)fabs(dot(pg, nf));
+      if (pa_front <= eps || pg_front <= eps) return nf;
+      atomicAdd(st_prism, 1ull);
+      float m = pa_bot;
+      if (pg_bot < m) m = pg_bot;
+      if (pa_right < m) m = pa_right;
+      if (pg_right < m) m = pg_right;
+      if (pa_front < m) m = pa_front;
+      if (pg_front < m) m = pg_front;
+      if (pa_bot == m || pg_bot == m) return nb;
+      if (pa_right == m || pg_right == m) return nr;
+      return nf;
+    }
+  }
+  return v3(0, 0, 0);
+}
+
+// GeoPrimitive::getUV (type 0/1/2)
+__device__ int shape_uv(int type, uint32_t flags, const double* __restrict__ g, V3 p, float shift,
+                        double& uo, double& vo)
+{
+  switch (type) {
+    case DT_SHAPE_RECTANGLE: {
+      V3 A, B, C, D;
+      if ((flags & DT_F_NAMED_RECT) && shift != 0.0f) shifted_rect(g, shift, A, B, C, D);
+      else { A = G3(g, RC_A); C = G3(g, RC_C); D = G3(g, RC_D); }
+      V3 ad = sub(D, A), dc = sub(C, D);
+      double nadc = ((flags & DT_F_NAMED_RECT) && shift != 0.0f) ? norm(ad) * norm(dc) : g[RC_NADC];
+      uo = (float)(norm(cross(sub(p, A), ad)) / nadc);
+      vo = (float)(norm(cross(sub(p, D), dc)) / nadc);
+      return 1;
+    }
+    case DT_SHAPE_RECTPRISM_V2: {
+      V3 A = G3(g, PR_F + R_A), ad = G3(g, PR_AD), dc = G3(g, PR_DC), D = G3(g, PR_D);
+      uo = (float)(norm(cross(sub(p, A), ad)) / g[PR_NADC]);
+      vo = (float)(norm(cross(sub(p, D), dc)) / g[PR_NADC]);
+      return 1;
+    }
+    case DT_SHAPE_TRIANGLE: {
+      V3 A = G3(g, TR_A), B = G3(g, TR_B), C = G3(g, TR_C);
+      V3 n = cross(sub(B, A), sub(C, A));
+      V3 n_a = cross(sub(C, B), sub(p, B));
+      V3 n_b = cross(sub(A, C), sub(p, C));
+      float nsq = (float)dot(n, n);
+      float al = (float)(dot(n, n_a) / nsq), be = (float)(dot(n, n_b) / nsq);
+      float ga = 1 - al - be;
+      if (al < 0 || al > 1 || be < 0 || be > 1 || ga < 0 || ga > 1) { uo = -1; vo = -1; return 0; }
+      uo = ((double)al * g[TR_UV + 0] + (double)be * g[TR_UV + 2]) + (double)ga * g[TR_UV + 4];
+      vo = ((double)al * g[TR_UV + 1] + (double)be * g[TR_UV + 3]) + (double)ga * g[TR_UV + 5];
+      return 1;
+    }
+    case DT_SHAPE_CHECKERBOARD_HOLE: {
+      V3 A = G3(g, CK_A), D = G3(g, CK_D);
+      V3 V_hit = sub(p, A);
+      float check1 = (float)dot(G3(g, CK_R + R_V1N), V_hit);
+      float check2 = (float)dot(G3(g, CK_R + R_V2N), V_hit);
+      if (0 <= check1 && check1 <= g[CK_R + R_LEN1] && 0 <= check2 && check2 <= g[CK_R + R_LEN2]) {
+        float tt, a, b;
+        if (rect_hit_R(g + CK_HOLE, v3(1, 1, 1), sub(p, v3(1, 1, 1)), 1e-4f, tt, a, b) && tt < FLT_MAX) {
+          uo = -1; vo = -1;
+          return 0;
+        }
+        V3 ad = G3(g, CK_AD), dc = G3(g, CK_DC);
+        float u = (float)(norm(cross(sub(p, A), ad)) / g[CK_NADC]);
+        float v = (float)(norm(cross(sub(p, D), dc)) / g[CK_NADC]);
+        float mud = (float)g[CK_MUD], mvd = (float)g[CK_MVD], bw = (float)g[CK_BW];
+        float miniu = u / mud - (int)(u / mud);
+        float miniv = v / mvd - (int)(v / mvd);
+        if (miniu < 0) miniu = 0;
+        if (miniv < 0) miniv = 0;
+        uo = miniu; vo = miniv;
+        if ((miniu <= bw || miniu >= 1 - bw) || (miniv <= bw || miniv >= 1 - bw)) return 2;
+        return 1;
+      }
+      uo = -1; vo = -1;
+      return 0;
+    }
+    case DT_SHAPE_CHECKER_CYLINDER: {
+      double ph[4] = {p.x, p.y, p.z, 1};
+      double po[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        double s = g[CY_M + i * 4 + 0] * ph[0];
+        s = s + g[CY_M + i * 4 + 1] * ph[1];
+        s = s + g[CY_M + i * 4 + 2] * ph[2];
+        s = s + g[CY_M + i * 4 + 3] * ph[3];
+        po[i] = s;
+      }
+      float u = 0;
+      if (p.x != 0) u = (float)((atan2(po[1], po[0]) + M_PI) / (2 * M_PI));
+      float v = (float)(po[2] / g[CY_NAX]);
+      float mud = (float)g[CY_MUD], mvd = (float)g[CY_MVD], bw = (float)g[CY_BW];
+      float miniu = u / mud - (int)(u / mud);
+      float miniv = v / mvd - (int)(v / mvd);
+      uo = miniu; vo = miniv;
+      if ((miniu <= bw || miniu >= 1 - bw) || (miniv <= bw || miniv >= 1 - bw)) return 2;
+      return 1;
+    }
+  }
+  uo = -1; vo = -1;
+  return 0;
+}
+
+// =====================================================================================
+// BVH: wave-uniform stackless traversal (geometry.cpp:2657-2740 box test)
+// =====================================================================================
+__device__ __forceinline__ bool box_hit(const DNode& b, float bump, V3 ray, V3 inv, V3 st)
+{
+  double lb1 = b.lb[1], ub1 = b.ub[1];
+  if (b.leaf && bump != 0.0f) { lb1 = lb1 - bump; ub1 = ub1 + bump; }   // bumpBVH (helpers.h:530)
+  float tmin, tmax;
+  if (isinf(inv.x)) {
+    if (!(st.x >= b.lb[0] && st.x <= b.ub[0])) return false;
+    tmin = FLT_MIN; tmax = FLT_MAX;
+  } else if (ray.x < 0) {
+    tmin = (float)((b.ub[0] - st.x) * inv.x);
+    tmax = (float)((b.lb[0] - st.x) * inv.x);
+  } else {
+    tmin = (float)((b.lb[0] - st.x) * inv.x);
+    tmax = (float)((b.ub[0] - st.x) * inv.x);
+  }
+  float tymin, tymax;
+  if (isinf(inv.y)) {
+    if (!(st.y >= lb1 && st.y <= ub1)) return false;
+    tymin = FLT_MIN; tymax = FLT_MAX;
+  } else if (ray.y < 0) {
+    tymin = (float)((ub1 - st.y) * inv.y);
+    tymax = (float)((lb1 - st.y) * inv.y);
+  } else {
+    tymin = (float)((lb1 - st.y) * inv.y);
+    tymax = (float)((ub1 - st.y) * inv.y);
+  }
+  if (tmin > tymax || tymin > tmax) return false;
+  if (tymin > tmin) tmin = tymin;
+  if (tymax < tmax) tmax = tymax;
+  float tzmin, tzmax;
+  if (isinf(inv.z)) {
+    if (!(st.z >= b.lb[2] && st.z <= b.ub[2])) return false;
+    tzmin = FLT_MIN; tzmax = FLT_MAX;
+  } else if (ray.z < 0) {
+    tzmin = (float)((b.ub[2] - st.z) * inv.z);
+    tzmax = (float)((b.lb[2] - st.z) * inv.z);
+  } else {
+    tzmin = (float)((b.lb[2] - st.z) * inv.z);
+    tzmax = (float)((b.ub[2] - st.z) * inv.z);
+  }
+  if (tmin > tzmax || tzmin > tmax) return false;
+  if (tzmin > tmin) tmin = tzmin;
+  if (tzmax < tmax) tmax = tzmax;
+  return tmax > 0;
+}
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+struct HitRec {
+  float t_min;
+  int shape;
+  int inside;
+  int has_ccol;
+  V3 ccol;
+};
+
+// closest hit over the lanes with `active` (cpp:491-538)
+__device__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 ray, V3 org, float shift,
+                            HitRec& h)
+{
+  V3 inv = v3(1.0 / ray.x, 1.0 / ray.y, 1.0 / ray.z);
+  int resume = active ? 0 : 0x7fffffff;
+  float t_dist = FLT_MAX;
+  bool any = false;
+  h.t_min = FLT_MAX;
+  h.shape = -1;
+  h.inside = 0;
+  h.has_ccol = 0;
+  int i = 0;
+  const int n_nodes = P.n_nodes;
+  while (i < n_nodes) {
+    const DNode nd = S.nodes[i];
+    bool act = resume <= i;
+    bool hb = act && box_hit(nd, shift, ray, inv, org);
+    if (nd.leaf) {
+      if (__ballot(hb)) {
+        for (int q = 0; q < nd.count; ++q) {
+          int sid = uni(S.leaf_idx[nd.first + q]);
+          DShapeHdr hd = S.hdr[sid];
+          if (hb) {
+            int ins = 0, hc = 0;
+            V3 cc;
+            if (shape_hit(S, sid, hd.type, hd.flags, S.geom + hd.off, ray, org, shift, t_dist, ins, cc, hc)) {
+              any = true;
+              if (t_dist < h.t_min) {
+                h.shape = sid;
+                h.inside = ins;
+                h.t_min = t_dist;
+                h.has_ccol = hc;
+                if (hc) h.ccol = cc;
+              }
+            }
+          }
+        }
+      }
+      if (act) resume = nd.skip;
+      i = i + 1;
+    } else {
+      if (act && !hb) resume = nd.skip;
+      i = __ballot(hb) ? i + 1 : nd.skip;
+    }
+  }
+  return any;
+}
+
+// any-hit shadow test (cpp:806-855): box test with sray from isectP+sray*1e-3, shape test
+// with normalized sray from isectP+sn*1e-3, skipping the light's own shape.
+__device__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
+                         V3 sstart, float t_max, int skip_shape, float shift)
+{
+  V3 inv = v3(1.0 / sray.x, 1.0 / sray.y, 1.0 / sray.z);
+  int resume = active ? 0 : 0x7fffffff;
+  bool occl = false;
+  int i = 0;
+  const int n_nodes = P.n_nodes;
+  while (i < n_nodes) {
+    const DNode nd = S.nodes[i];
+    bool act = resume <= i;
+    bool hb = act && box_hit(nd, shift, sray, inv, bstart);
+    if (nd.leaf) {
+      if (__ballot(hb)) {
+        for (int q = 0; q < nd.count; ++q) {
+          int sid = uni(S.leaf_idx[nd.first + q]);
+          DShapeHdr hd = S.hdr[sid];
+          if (hb && !occl && sid != skip_shape) {
+            if (shape_shadow(hd.type, hd.flags, S.geom + hd.off, sn, sstart, t_max, shift)) occl = true;
+          }
+        }
+      }
+      if (act) resume = occl ? 0x7fffffff : nd.skip;
+      i = i + 1;
+    } else {
+      if (act && !hb) resume = nd.skip;
+      i = __ballot(hb) ? i + 1 : nd.skip;
+    }
+    if (!__ballot(resume != 0x7fffffff)) break;
+  }
+  return occl;
+}
+
+// =====================================================================================
+// rayColor as a per-lane DFS (render_final_project.cpp:487-961)
+// =====================================================================================
+struct Entry {
+  V3 a;        // NODE: ray     FINISH: colour to add
+  V3 b;        // NODE: origin
+  float k;
+  int depth;   // >0 NODE ; -1 FINISH
+  uint32_t key;
+  int _pad;
+};
+
+struct PassOut {
+  V3 color;
+  bool hit;
+  bool in_motion;
+};
+
+struct Ctx {
+  const DScene* S;
+  const DParams* P;
+  Rng rng;
+};
+
+__device__ __forceinline__ bool is_refl_material(int m)
+{
+  return m == DT_MAT_GLASS || m == DT_MAT_STEEL || m == DT_MAT_ALUMINUM || m == DT_MAT_WATER ||
+         m == DT_MAT_LINOLEUM;
+}
+
+// glossy sample rectangle (cpp:648-669 / 742-755)
+__device__ void glossy_rect(V3 refl_ray, V3 isectP, float mult, V3& A, V3& B, V3& C, V3& D, V3& wv, V3& lv)
+{
+  const float length = 1, width = 0.5;
+  V3 gloss_ray = mul(mult, refl_ray);
+  lv = normalized(cross(gloss_ray, v3(1, 0, 0)));
+  if (is_approx_zero(lv)) lv = cross(gloss_ray, v3(0, 0, 1));
+  V3 cc = add(gloss_ray, isectP);
+  V3 p1 = add(mul(length / 2, lv), cc);
+  wv = normalized(cross(neg(gloss_ray), lv));
+  A = add(divs(mul(width, wv), 2), p1);
+  B = sub(A, mul(length, lv));
+  C = sub(B, mul(width, wv));
+  D = sub(A, mul(width, wv));
+}
+
+__device__ __forceinline__ V3 rect_sample(V3 A, V3 B, V3 D, double u0, double u1)
+{
+  float x = (float)u0, y = (float)u1;
+  return add(add(A, mul(x, sub(B, A))), mul(y, sub(D, A)));
+}
+
+// light sampleRay (geometry.cpp:2751-2849)
+__device__ V3 light_sample(const Ctx& c, const DLight& L, int li, V3 point, uint32_t node,
+                           unsigned long long* st_sphl)
+{
+  if (L.type == DT_LIGHT_POINT) return sub(v3a(L.center), point);
+  if (L.type == DT_LIGHT_RECT) {
+    double u0, u1;
+    c.rng.draw(node, P_LIGHT, (uint32_t)li, u0, u1);
+    return sub(rect_sample(v3a(L.A), v3a(L.B), v3a(L.D), u0, u1), point);
+  }
+  V3 C = v3a(L.center), baxis = v3a(L.baxis);
+  int attempt = 0;
+  double u0, u1;
+  c.rng.draw(node, P_SPHL, ((uint32_t)li << 8) | (uint32_t)attempt, u0, u1);
+  double theta = 2 * M_PI * u0, phi = acos(1 - 2 * u1);
+  V3 dir = v3(sin(phi) * cos(theta), sin(phi) * sin(theta), cos(phi));
+  V3 tmp = add(mul(L.radius, dir), C);
+  int sample_limit = 20;
+  while (dot(sub(tmp, C), sub(point, C)) < 0 || (L.use_baxis && dot(sub(tmp, C), baxis) < 0)) {
+    if (sample_limit < 0) { atomicAdd(st_sphl, 1ull); break; }
+    V3 rev = add(mul(-L.radius, dir), C);
+    if (dot(sub(rev, C), sub(point, C)) >= 0 && (!L.use_baxis || dot(sub(rev, C), baxis) >= 0)) {
+      tmp = rev;
+      break;
+    }
+    attempt++;
+    c.rng.draw(node, P_SPHL, ((uint32_t)li << 8) | (uint32_t)attempt, u0, u1);
+    theta = 2 * M_PI * u0;
+    phi = acos(1 - 2 * u1);
+    dir = v3(sin(phi) * cos(theta), sin(phi) * sin(theta), cos(phi));
+    tmp = add(mul(L.radius, dir), C);
+    sample_limit--;
+  }
+  return tmp;
+}
+
+// helpers.h:313-317 (Q10)
+__device__ __forceinline__ float schlick_complex(float cos_theta, double r0, double r1)
+{
+  float R0 = (float)((pow(r0 - 1, 2.0) + pow(r1, 2.0)) / (pow(r0 + 1, 2.0) + pow(r1, 2.0)));
+  return (float)((R0 + (1 - R0)) + pow((double)(1 - cos_theta), 5.0));
+}
+
+// One full rayColor tree for the lanes with `active`. Appends to out.color in the
+// reference's accumulation order.
+__device__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t rootkey, float shift,
+                         PassOut& out, Entry* stack)
+{
+  const DScene& S = *c.S;
+  const DParams& P = *c.P;
+  int sp = 0;
+  if (active && P.max_depth > 0) {
+    Entry e;
+    e.a = ray0; e.b = org0; e.k = 1.0f; e.depth = P.max_depth; e.key = rootkey; e._pad = 1;  // root
+    stack[sp++] = e;
+  }
+  unsigned long long n_rays = 0, n_shadow = 0;
+  while (true) {
+    // pop FINISH entries (own-light contributions), then the next NODE
+    bool have = false;
+    Entry e;
+    while (sp > 0) {
+      e = stack[--sp];
+      if (e.depth < 0) {
+        out.color = add(out.color, e.a);
+      } else {
+        have = true;
+        break;
+      }
+    }
+    if (!__ballot(have)) break;
+    const V3 ray = e.a, eye = e.b;
+    const int depth = e.depth;
+    const float k = e.k;
+    const uint32_t node = e.key;
+    const bool is_root = have && e._pad == 1;
+    if (have) { out.in_motion = false; n_rays++; }   // cpp:519
+
+    HitRec h;
+    bool any = closest_hit(S, P, have, ray, eye, shift, h);
+    any = any && have && h.shape >= 0;
+    if (have && is_root && any) out.hit = true;
+
+    // ---- per-lane hit processing: normal, reflection children (cpp:546-769) ----------
+    V3 isectP = v3(0, 0, 0), normal = v3(0, 0, 0), in = v3(0, 0, 0), shape_color = v3(0, 0, 0);
+    int sid = any ? h.shape : 0;
+    DShapeHdr hd;
+    hd.type = 0; hd.off = 0; hd.flags = 0;
+    int fin_slot = -1;
+    bool shade = false;     // needs the light loop
+    V3 own = v3(0, 0, 0);
+    if (any) {
+      hd = S.hdr[sid];
+      const double* g = S.geom + hd.off;
+      const DMat& M = S.mat[sid];
+      isectP = add(eye, mul(h.t_min, ray));
+      normal = shape_norm(hd.type, hd.flags, g, isectP, shift, S.stats + ST_PRISM);
+      in = normalized(ray);
+      shape_color = h.has_ccol ? h.ccol : v3a(M.color);
+      out.in_motion = (M.flags & DT_F_MOTION) != 0;
+      if (dot(mul(1e4, in), normal) >= 0) normal = mul(-1, normal);   // fixNorm
+
+      // reserve the FINISH slot below the children
+      if (sp < DT_STACK_MAX) { fin_slot = sp++; }
+      else atomicAdd(S.stats + ST_STACK, 1ull);
+
+      if (P.reflect && is_refl_material(M.material)) {
+        const float eps = 1e-3f;
+        const bool glossy = (M.flags & DT_F_GLOSSY) != 0;
+        float k_refl = 1, k_refr = 1;
+        // children are pushed in reverse call order after being generated in call order
+        Entry kids[8];
+        int nk = 0;
+        if (M.material == DT_MAT_GLASS) {
+          float cos_theta = (float)dot(normal, neg(in));
+          float sin_theta = (float)sqrt(1 - pow((double)cos_theta, 2.0));
+          float r1 = h.inside ? P.refr_glass : P.refr_air, r2 = h.inside ? P.refr_air : P.refr_glass;
+          float chk = (float)(1 - pow((double)(r1 / r2), 2.0) * (1 - pow(dot(in, normal), 2.0)));
+          if (chk >= 0) {
+            float a = r1 / r2 * sin_theta;
+            float b = 1 / sin_theta;
+            float sq = sqrtf(chk);
+            V3 outr = sub(mul(a, mul(b, add(in, mul(cos_theta, normal)))), mul(sq, normal));
+            V3 adj_org = add(isectP, mul(eps, in));
+            float cos_phi = (float)sqrt(1 - pow((double)(P.refr_glass / P.refr_air), 2.0) *
+                                                (1 - pow(dot(in, normal), 2.0)));
+            float rp = (P.refr_glass * cos_theta - P.refr_air * cos_phi) /
+                       (P.refr_glass * cos_theta + P.refr_air * cos_phi);
+            float rs = (P.refr_air * cos_theta - P.refr_glass * cos_phi) /
+                       (P.refr_air * cos_theta + P.refr_glass * cos_phi);
+            k_refl = (float)(0.5 * (pow((double)rp, 2.0) + pow((double)rs, 2.0)));
+            k_refr = 1 - k_refl;
+            Entry ch; ch.a = outr; ch.b = adj_org; ch.k = k_refr * k; ch.depth = depth - 1;
+            ch.key = child_key(node, 0); ch._pad = 0;
+            kids[nk++] = ch;
+          }
+        }
+        V3 refl_ray = sub(in, mul(2 * dot(normal, in), normal));
+        if (dot(refl_ray, normal) <= 0) {
+          atomicAdd(S.stats + ST_REFL, 1ull);
+        } else if (dot(refl_ray, normal) > eps) {
+          if (glossy && !P.nogloss) {
+            V3 A, B, C, D, wv, lv;
+            glossy_rect(refl_ray, isectP, 2.0f, A, B, C, D, wv, lv);
+            V3 wa = wv, la = lv;
+            if (dot(wv, normal) <= 0) wa = neg(wa);
+            if (dot(lv, normal) <= 0) la = neg(la);
+            // squeeze (cpp:680-695); bounded so a degenerate normal cannot hang the GPU
+            for (int it = 0; it < 100000 && dot(sub(A, isectP), normal) <= 0; ++it) A = add(add(A, mul(0.1, wa)), mul(0.1, la));
+            for (int it = 0; it < 100000 && dot(sub(B, isectP), normal) <= 0; ++it) B = add(add(B, mul(0.1, wa)), mul(0.1, la));
+            for (int it = 0; it < 100000 && dot(sub(C, isectP), normal) <= 0; ++it) C = add(add(C, mul(0.1, wa)), mul(0.1, la));
+            for (int it = 0; it < 100000 && dot(sub(D, isectP), normal) <= 0; ++it) D = add(add(D, mul(0.1, wa)), mul(0.1, la));
+            for (int i = 0; i < P.brdf_samples && nk < 8; i++) {
+              int attempt = 0;
+              double u0, u1;
+              c.rng.draw(node, P_GLOSSY, ((uint32_t)i << 8) | (uint32_t)attempt, u0, u1);
+              V3 sample_refl = sub(rect_sample(A, B, D, u0, u1), isectP);
+              int sample_limit = 10;
+              bool exhausted = false;
+              while (dot(sample_refl, normal) <= 0) {
+                if (sample_limit < 0) { exhausted = true; break; }
+                float multiplier = (float)pow(2.0, (double)(11 - sample_limit));
+                glossy_rect(refl_ray, isectP, multiplier, A, B, C, D, wv, lv);
+                attempt++;
+                c.rng.draw(node, P_GLOSSY, ((uint32_t)i << 8) | (uint32_t)attempt, u0, u1);
+                sample_refl = sub(rect_sample(A, B, D, u0, u1), isectP);
+                sample_limit--;
+              }
+              if (exhausted) { atomicAdd(S.stats + ST_GLOSSY, 1ull); continue; }
+              Entry ch; ch.a = sample_refl; ch.b = add(isectP, mul(eps, sample_refl));
+              ch.k = k_refl * k / P.brdf_samples; ch.depth = depth - 1; ch.key = child_key(node, 2 + i);
+              ch._pad = 0;
+              kids[nk++] = ch;
+            }
+          } else {
+            Entry ch; ch.a = refl_ray; ch.b = add(isectP, mul(eps, refl_ray)); ch.k = k_refl * k;
+            ch.depth = depth - 1; ch.key = child_key(node, 1); ch._pad = 0;
+            kids[nk++] = ch;
+          }
+        }
+        if (depth - 1 > 0) {
+          for (int q = nk - 1; q >= 0; --q) {
+            if (sp < DT_STACK_MAX) stack[sp++] = kids[q];
+            else atomicAdd(S.stats + ST_STACK, 1ull);
+          }
+        }
+      }
+
+      // emissive (cpp:775-789)
+      if (M.flags & DT_F_LIGHT) {
+        if (M.emit == DT_EMIT_SPHERE) {
+          float hitdot = (float)dot(in, normalized(sub(v3a(M.center), isectP)));
+          double f = (0.1 * pow((double)hitdot, 1.0) + 0.05 * pow((double)hitdot, 5.0)) + 0.9;
+          own = mul(f, mul(k, shape_color));
+        }
+        if (M.emit == DT_EMIT_RECT) {
+          V3 A = G3(g, RC_A), B = G3(g, RC_B), C = G3(g, RC_C), D = G3(g, RC_D);
+          float dist = (float)((((norm(sub(isectP, A)) + norm(sub(isectP, B))) + norm(sub(isectP, C))) +
+                                norm(sub(isectP, D))) /
+                               (8 * norm(sub(v3a(M.center), A))));
+          double f = (0.1 * pow((double)dist, 1.0) + 0.05 * pow((double)dist, 5.0)) + 0.9;
+          own = mul(f, mul(k, shape_color));
+        }
+      } else {
+        shade = true;
+      }
+    }
+
+    // ---- direct lighting: uniform loop over lights, packet shadow rays (cpp:800-959) ----
+    if (__ballot(shade)) {
+      const DMat* Mp = S.mat + sid;
+      V3 e_dir = normalized(sub(eye, isectP));
+      int hits = 0;
+      bool aborted = false;
+      V3 tmp_color = v3(0, 0, 0);
+      for (int li = 0; li < P.n_lights; ++li) {
+        const DLight L = S.lights[li];
+        bool lane = shade && !aborted;
+        V3 sray = v3(1, 0, 0);
+        float t_max = 0;
+        V3 sn = v3(1, 0, 0);
+        if (lane) {
+          sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL);
+          t_max = (float)norm(sray);
+          sn = normalized(sray);
+          n_shadow++;
+        }
+        bool occl = occluded(S, P, lane, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
+                             t_max, L.shape_index, shift);
+        if (lane && !occl) {
+          const DMat& M = *Mp;
+          const double* g = S.geom + hd.off;
+          V3 lc = v3a(L.color);
+          V3 r = normalized(add(mul(-1, sray), mul(2 * dot(normal, sray), normal)));
+          bool skip_rest = false;
+          if (M.flags & DT_F_TEXTURE) {
+            double u, v;
+            int type = shape_uv(hd.type, hd.flags, g, isectP, shift, u, v);
+            if (type == 0) {
+              aborted = true;   // Q8: `return` discards this node's lighting
+              skip_rest = true;
+            } else {
+              if (u < 0 || v < 0 || u > 1 || v > 1) atomicAdd(S.stats + ST_UV, 1ull);
+              if (type == 2) {
+                shape_color = v3a(M.bordercolor);
+              } else if (type == 1 && M.tex >= 0) {
+                double dims0 = M.tex_w;
+                int x_tex = (int)((float)(M.tex_w - 1) * (float)u);
+                int y_tex = (int)((float)(M.tex_h - 1) * (float)v);
+                int uv_ind = (int)(y_tex * dims0 + x_tex);
+                if (uv_ind < 0) uv_ind = 0;
+                if (uv_ind >= M.tex_w * M.tex_h) uv_ind = M.tex_w * M.tex_h - 1;
+                const uint8_t* px = S.tex + M.tex_off + (int64_t)uv_ind * M.tex_ch;
+                shape_color = v3(px[0] / 255.0, px[1] / 255.0, px[2] / 255.0);
+              }
+            }
+          }
+          if (!skip_rest) {
+            V3 ray_col;
+            const float roughness = M.roughness;
+            if (M.model == DT_MODEL_OREN_NAYAR) {
+              float A = (float)(1.0 - (0.5 * pow((double)roughness, 2.0)) / (pow((double)roughness, 2.0) + 0.33));
+              float B = (float)((0.45 * pow((double)roughness, 2.0)) / (pow((double)roughness, 2.0) + 0.09));
+              float vn = (float)dot(e_dir, normal);
+              float ln = (float)dot(sn, normal);
+              float irradiance = fmaxr(0.0f, ln);
+              float vn_theta = acosf(vn), ln_theta = acosf(ln);
+              float angleDiff = (float)dmax(0.0, dot(normalized(sub(e_dir, mul(vn, normal))),
+                                                     normalized(sub(sray, mul(ln, normal)))));
+              float alpha = fmaxr(vn_theta, ln_theta), beta = fminr(vn_theta, ln_theta);
+              float f = A + B * angleDiff * sinf(alpha) * tanf(beta);
+              ray_col = mul(f, mul(irradiance, cwise(shape_color, lc)));
+            } else if (M.model == DT_MODEL_COOK_TORRANCE) {
+              V3 H = normalized(add(e_dir, sray));
+              float hn = (float)dmax(0.0, dot(normal, H));
+              float vh = (float)dot(e_dir, H);
+              float vn = (float)dot(e_dir, normal);
+              float ln = (float)dot(sn, normal);
+              float alpha = acosf(hn);
+              float D = (float)(1 / (pow((double)roughness, 2.0) * pow((double)cosf(alpha), 4.0)) *
+                                exp(-pow((double)(tanf(alpha) / roughness), 2.0)));
+              float G1 = (float)(2.0 * hn * vn / vh);
+              float G2 = (float)(2.0 * hn * ln / vh);
+              float G = 1.0f;
+              if (G1 < G) G = G1;
+              if (G2 < G) G = G2;
+              float F = schlick_complex(vn, M.refr[0], M.refr[1]);
+              float fdg = F * D * G;
+              double den = (double)(ln * vn) * M_PI;
+              V3 shader_rgb = add(mul(fmaxr(0.0f, ln), mul(0.4, lc)), divs(mul(fdg, mul(0.8, lc)), den));
+              ray_col = cwise(shape_color, shader_rgb);
+            } else if (M.model == DT_MODEL_RAW) {
+              ray_col = shape_color;
+            } else {
+              double m1 = dmax(0.0, dot(normal, sn));
+              double pp = pow(dmax(0.0, dot(r, e_dir)), (double)P.phong);
+              V3 shader_rgb = add(mul(m1, lc), mul(pp, lc));
+              ray_col = cwise(shape_color, shader_rgb);
+            }
+            if (!is_approx_zero(ray_col)) {
+              hits++;
+              tmp_color = add(tmp_color, mul(k, ray_col));
+            }
+          }
+        }
+      }
+      if (shade && !aborted && hits > 0) own = divs(tmp_color, hits);
+    }
+    if (fin_slot >= 0) {
+      Entry f;
+      f.a = own; f.b = v3(0, 0, 0); f.k = 0; f.depth = -1; f.key = 0; f._pad = 0;
+      stack[fin_slot] = f;
+    }
+  }
+  if (n_rays) atomicAdd(S.stats + ST_RAYS, n_rays);
+  if (n_shadow) atomicAdd(S.stats + ST_SHADOW, n_shadow);
+}
+
+// =====================================================================================
+// render kernel: persistent waves over pixel groups
+// =====================================================================================
+__device__ __forceinline__ void pixel_of(const DParams& P, int64_t q, int& x, int& y, int64_t& slab_off,
+                                         bool& valid)
+{
+  const int64_t tile_px = (int64_t)P.tw * P.th;
+  int64_t slot = q / tile_px;
+  int local = (int)(q - slot * tile_px);
+  int py = local / P.tw, px = local - py * P.tw;
+  int64_t t = (int64_t)P.rank + slot * P.world;
+  int ty = (int)(t / P.tiles_x), tx = (int)(t - (int64_t)ty * P.tiles_x);
+  x = P.x0 + tx * P.tw + px;
+  y = P.y0 + ty * P.th + py;
+  valid = slot < P.n_owned_tiles && x < P.x1 && y < P.y1;
+  slab_off = q * 3;
+}
+
+__device__ __forceinline__ void store_pixel(const DParams& P, float* out, int x, int y, int64_t slab_off, V3 color)
+{
+  int64_t off = P.layout == DT_OUT_SLAB ? slab_off : 3 * ((int64_t)(P.yRes - 1 - y) * P.xRes + x);
+  out[off + 0] = clampf01((float)color.x) * 255.0f;
+  out[off + 1] = clampf01((float)color.y) * 255.0f;
+  out[off + 2] = clampf01((float)color.z) * 255.0f;
+}
+
+struct DLaunch {
+  DScene S;
+  DParams P;
+};
+
+extern "C" __global__ void __launch_bounds__(64)
+dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
+{
+  const DScene& S = Lp->S;
+  const DParams& P = Lp->P;
+  __shared__ double red[DT_WAVE * 3];
+  __shared__ float dens[DT_MAX_CLOUD_STEPS];
+  __shared__ double chan[4];
+  __shared__ unsigned long long item_s;
+  Entry stack[DT_STACK_MAX];
+  const int lane = threadIdx.x;
+  Ctx c;
+  c.S = &S;
+  c.P = &P;
+  c.rng.k0 = P.seed;
+  c.rng.k1 = (uint32_t)P.frame;
+  unsigned long long sky_px = 0;
+
+  while (true) {
+    if (lane == 0) item_s = atomicAdd(S.queue, 1ull);
+    __syncthreads();
+    const int64_t item = (int64_t)item_s;
+    __syncthreads();
+    if (item >= P.n_items) break;
+
+    const int group = P.ppw;
+    const int spp = P.spp;
+    // lanes: pixel slot j = lane / min(spp,64), sample = chunk*64 + lane % ...
+    const int per = spp < DT_WAVE ? spp : DT_WAVE;
+    const int j = lane / per;
+    V3 pix_sum = v3(0, 0, 0);   // lane j (< group) accumulates pixel j in sample order
+    int px_x = 0, px_y = 0;
+    int64_t px_off = 0;
+    bool px_valid = false;
+    pixel_of(P, item * group + (j < group ? j : 0), px_x, px_y, px_off, px_valid);
+
+    for (int chunk = 0; chunk < P.chunks; ++chunk) {
+      const int sample = chunk * DT_WAVE + (lane - j * per);
+      const bool valid = j < group && px_valid && sample < spp && (lane - j * per) < per;
+      c.rng.pixel = (uint32_t)(px_y * P.xRes + px_x);
+      c.rng.sample = (uint32_t)sample;
+
+      // camera ray (cpp:1044-1072)
+      V3 eye = v3a(P.eye), X = v3a(P.X), Y = v3a(P.Y), Z = v3a(P.Z);
+      V3 eye_sample = eye;
+      if (P.aperture > 0) {
+        double u0, u1;
+        c.rng.draw(0, P_DOF, 0, u0, u1);
+        float r = (float)(P.aperture / 2 * u0);
+        float theta = (float)(2 * M_PI * u1);
+        eye_sample = add(add(eye, mul(r * cosf(theta), X)), mul(r * sinf(theta), Y));
+      }
+      float a = P.l + (P.r - P.l) * (float)px_x / (float)P.xRes;
+      float b = P.b + (P.t - P.b) * (float)px_y / (float)P.yRes;
+      V3 rayDir = sub(add(mul(a, X), mul(b, Y)), mul(P.near_plane, Z));
+      V3 focalPoint = add(eye, mul(P.focal_length, rayDir));
+      V3 ray0 = sub(focalPoint, eye_sample);
+
+      PassOut po;
+      po.color = v3(0, 0, 0);
+      po.hit = false;
+      po.in_motion = false;
+      run_pass(c, valid, ray0, eye_sample, root_key(0), 0.0f, po, stack);
+      V3 tmp_color = po.color;
+      const bool need_blur = valid && po.hit && po.in_motion;
+      if (__ballot(need_blur)) {   // motion blur re-traces (cpp:1095-1210)
+        for (int m = 0; m < P.blur_samples; ++m) {
+          float val = 0.0f;
+          if (need_blur) {
+            double u0, u1;
+            c.rng.draw(0, P_BLUR, (uint32_t)m, u0, u1);
+            float frame_sample = (float)((float)P.frame + u0 * P.frame_range);
+            if (P.frame >= P.frame_prism) {
+              if (P.frame >= P.frame_blur)
+                val = (float)(P.move_per_frame * (frame_sample - P.frame) +
+                              P.accel_t * pow((double)(frame_sample - P.frame), 3.0));
+              else
+                val = P.move_per_frame * (frame_sample - P.frame);
+            }
+          }
+          PassOut pm;
+          pm.color = v3(0, 0, 0);
+          pm.hit = true;
+          pm.in_motion = false;
+          run_pass(c, need_blur, ray0, eye_sample, root_key(m + 1), val, pm, stack);
+          if (need_blur) tmp_color = add(tmp_color, pm.color);
+        }
+        if (need_blur) tmp_color = divs(tmp_color, P.blur_samples + 1);
+      }
+      const bool miss = valid && !po.hit;
+      // sky for missing samples: computed once per pixel by the whole wave
+      if (P.perlin_cloud) {
+        for (int jj = 0; jj < group; ++jj) {
+          if (__ballot(miss && j == jj)) {
+            int qx, qy;
+            int64_t qo;
+            bool qv;
+            pixel_of(P, item * group + jj, qx, qy, qo, qv);
+            float aa = P.l + (P.r - P.l) * (float)qx / (float)P.xRes;
+            float bb = P.b + (P.t - P.b) * (float)qy / (float)P.yRes;
+            V3 rd = sub(add(mul(aa, X), mul(bb, Y)), mul(P.near_plane, Z));
+            V3 fp = add(eye, mul(P.focal_length, rd));
+            V3 pt;
+            pt.x = ((P.sky_m[0][0] * fp.x + P.sky_m[0][1] * fp.y) + P.sky_m[0][2] * fp.z) + P.sky_m[0][3] * 1.0;
+            pt.y = ((P.sky_m[1][0] * fp.x + P.sky_m[1][1] * fp.y) + P.sky_m[1][2] * fp.z) + P.sky_m[1][3] * 1.0;
+            pt.z = ((P.sky_m[2][0] * fp.x + P.sky_m[2][1] * fp.y) + P.sky_m[2][2] * fp.z) + P.sky_m[2][3] * 1.0;
+            V3 skyc = cloud_color_coop(P, S.cloud_z, pt, dens, chan);
+            if (miss && j == jj) tmp_color = skyc;
+            if (lane == 0) sky_px++;
+          }
+        }
+      } else if (miss) {
+        tmp_color = v3a(P.default_col);
+      }
+      // ordered per-pixel sum (cpp:1212: color += tmp_color in sample order)
+      red[lane * 3 + 0] = tmp_color.x;
+      red[lane * 3 + 1] = tmp_color.y;
+      red[lane * 3 + 2] = tmp_color.z;
+      __syncthreads();
+      if (lane < group) {
+        const int base = lane * per;
+        int ns = spp - chunk * DT_WAVE;
+        if (ns > per) ns = per;
+        for (int s = 0; s < ns; ++s)
+          pix_sum = add(pix_sum, v3(red[(base + s) * 3], red[(base + s) * 3 + 1], red[(base + s) * 3 + 2]));
+      }
+      __syncthreads();
+    }
+    if (lane < group) {
+      int qx, qy;
+      int64_t qo;
+      bool qv;
+      pixel_of(P, item * group + lane, qx, qy, qo, qv);
+      if (qv) {
+        V3 color = divs(pix_sum, spp);
+        store_pixel(P, out, qx, qy, qo, color);
+        if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
+      }
+    }
+  }
+  if (lane == 0 && sky_px) atomicAdd(S.stats + ST_SKY, sky_px);
+}
+
+// renderImageCloud (cpp:1224-1279): one pixel per lane
+extern "C" __global__ void __launch_bounds__(256)
+dt_sky_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
+{
+  const DParams& P = Lp->P;
+  const float* __restrict__ zs = Lp->S.cloud_z;
+  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = P.n_owned_tiles * P.tw * P.th;
+  if (q >= total) return;
+  int x, y;
+  int64_t so;
+  bool valid;
+  pixel_of(P, q, x, y, so, valid);
+  if (!valid) return;
+  V3 eye = v3a(P.eye), X = v3a(P.X), Y = v3a(P.Y), Z = v3a(P.Z);
+  float a = P.l + (P.r - P.l) * (float)x / (float)P.xRes;
+  float b = P.b + (P.t - P.b) * (float)y / (float)P.yRes;
+  V3 rayDir = sub(add(mul(a, X), mul(b, Y)), mul(P.near_plane, Z));
+  V3 fp = add(rayDir, eye);
+  V3 pt;
+  pt.x = ((P.sky_m[0][0] * fp.x + P.sky_m[0][1] * fp.y) + P.sky_m[0][2] * fp.z) + P.sky_m[0][3] * 1.0;
+  pt.y = ((P.sky_m[1][0] * fp.x + P.sky_m[1][1] * fp.y) + P.sky_m[1][2] * fp.z) + P.sky_m[1][3] * 1.0;
+  pt.z = ((P.sky_m[2][0] * fp.x + P.sky_m[2][1] * fp.y) + P.sky_m[2][2] * fp.z) + P.sky_m[2][3] * 1.0;
+  V3 color = cloud_color_lane(P, zs, pt);
+  store_pixel(P, out, x, y, so, color);
+}
+
+// slab -> image scatter (multi-GPU gather epilogue)
+extern "C" __global__ void dt_unpack_kernel(const DLaunch* __restrict__ Lp, int world, int64_t slab_floats,
+                                            const float* __restrict__ slabs, float* __restrict__ image)
+{
+  const DParams& P = Lp->P;
+  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over rank-major slab pixels
+  int64_t per_rank = slab_floats / 3;
+  int64_t total = per_rank * world;
+  if (q >= total) return;
+  int r = (int)(q / per_rank);
+  int64_t local = q - (int64_t)r * per_rank;
+  int64_t ntiles = (int64_t)P.tiles_x * ((P.y1 - P.y0 + P.th - 1) / P.th);
+  int64_t owned = ntiles > r ? (ntiles - r + world - 1) / world : 0;
+  const int64_t tile_px = (int64_t)P.tw * P.th;
+  int64_t slot = local / tile_px;
+  int lp = (int)(local - slot * tile_px);
+  int py = lp / P.tw, px = lp - py * P.tw;
+  int64_t t = (int64_t)r + slot * world;
+  int ty = (int)(t / P.tiles_x), tx = (int)(t - (int64_t)ty * P.tiles_x);
+  int x = P.x0 + tx * P.tw + px, y = P.y0 + ty * P.th + py;
+  bool valid = slot < owned && x < P.x1 && y < P.y1;
+  if (!valid) return;
+  int64_t off = 3 * ((int64_t)(P.yRes - 1 - y) * P.xRes + x);
+  const float* s = slabs + (int64_t)r * slab_floats + local * 3;
+  image[off] = s[0];
+  image[off + 1] = s[1];
+  image[off + 2] = s[2];
+}
+
+// ---- host-side launch wrappers ---------------------------------------------------------
+extern "C" size_t dt_launch_size(void) { return sizeof(DLaunch); }
+extern "C" size_t dt_scene_struct_offset(void) { return offsetof(DLaunch, S); }
+extern "C" size_t dt_params_struct_offset(void) { return offsetof(DLaunch, P); }
+
+extern "C" hipError_t dt_launch_trace(const void* dev_launch, float* out, int grid, hipStream_t stream)
+{
+  hipLaunchKernelGGL(dt_trace_kernel, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
+  return hipGetLastError();
+}
+extern "C" hipError_t dt_launch_sky(const void* dev_launch, float* out, int64_t n_threads, hipStream_t stream)
+{
+  int64_t blocks = (n_threads + 255) / 256;
+  hipLaunchKernelGGL(dt_sky_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const DLaunch*)dev_launch, out);
+  return hipGetLastError();
+}
+extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_t slab_floats, const float* slabs,
+                                       float* image, hipStream_t stream)
+{
+  int64_t total = slab_floats / 3 * world;
+  int64_t blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(dt_unpack_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const DLaunch*)dev_launch,
+                     world, slab_floats, slabs, image);
+  return hipGetLastError();
+}
+extern "C" const void* dt_trace_kernel_ptr(void) { return (const void*)dt_trace_kernel; }

@@ -1,0 +1,114 @@
+// dt_scene_dev.h — device-resident scene layout (host flattener <-> HIP kernels).
+//
+// Layout in HBM (all arrays are tiny next to the 288 GB; the whole scene of the default
+// frame is ~60 KB and lives in L2/scalar cache during a render):
+//   nodes[]    BVH in the reference's traversal order (pre-order, last child first,
+//              render_final_project.cpp:491-512), with skip links -> stackless,
+//              wave-uniform traversal (each wave walks the union of its lanes' paths).
+//   leaf_idx[] shape indices of each leaf, in leaf order.
+//   hdr[]      per-shape {type, geom offset, flags}; read with a wave-uniform index.
+//   geom[]     per-shape doubles, layout per type below; every value is computed on the host
+//              with the same IEEE operation sequence the reference performs per call
+//              (e.g. Rectangle::intersect's getNorm(start).normalized()), so precomputation
+//              changes no bit of any result.
+//   mat[]      per-shape shading record; read with a per-lane index (hit shape).
+//   lights[]   light records.
+//   tex[]      RGB8 texel pool (stb_image bytes; the renderer uses byte/255.0).
+#pragma once
+#include <stdint.h>
+
+namespace dtd {
+
+struct alignas(16) DNode {
+  double lb[3];
+  double ub[3];
+  int32_t skip;   // index of the first node after this subtree
+  int32_t leaf;
+  int32_t first;  // leaf: first entry in leaf_idx
+  int32_t count;  // leaf: number of shapes
+};
+
+struct alignas(16) DShapeHdr {
+  int32_t type;
+  int32_t off;     // offset into geom[] (doubles)
+  uint32_t flags;  // DT_F_*
+  int32_t _pad;
+};
+
+struct alignas(16) DMat {
+  int32_t model, material, emit;
+  uint32_t flags;
+  int32_t tex;     // texture index or -1
+  int32_t tex_w, tex_h, tex_ch;
+  int64_t tex_off; // byte offset into tex pool
+  float roughness, radius;
+  double refr[2];
+  double color[3];
+  double bordercolor[3];
+  double center[3];
+};
+
+struct alignas(16) DLight {
+  int32_t type, shape_index, use_baxis, _pad;
+  double radius;
+  double center[3], color[3], baxis[3], A[3], B[3], D[3];
+};
+
+// ---- geometry record layouts (offsets in doubles) ----------------------------------------
+// Rectangle plane record R (Rectangle::intersect/intersectShadow, geometry.cpp:640-741):
+//   n   = normalized(normalized((B-A) x (C-A)))   (getNorm(start).normalized())
+//   V1n = normalized(B-A), V2n = normalized(D-A), len1 = |B-A|, len2 = |D-A|
+enum { R_A = 0, R_N = 3, R_V1N = 6, R_V2N = 9, R_LEN1 = 12, R_LEN2 = 13, R_SIZE = 14 };
+
+// SPHERE: center, r2 = pow(radius,2)
+enum { SP_C = 0, SP_R2 = 3, SP_SIZE = 4 };
+// CYLINDER / CHECKER_CYLINDER: c1, c2, axis = normalized(c2-c1), r2; UV block for checker:
+//   objM rows 0..2 (12), |axis|, miniu_dist, miniv_dist, bw (floats stored as double)
+enum { CY_C1 = 0, CY_C2 = 3, CY_AX = 6, CY_R2 = 9, CY_M = 10, CY_NAX = 22, CY_MUD = 23,
+       CY_MVD = 24, CY_BW = 25, CY_SIZE = 26 };
+// TRIANGLE: A, B, C, r1 = B-A, r2 = C-A, mesh_normal, uvA, uvB, uvC
+enum { TR_A = 0, TR_B = 3, TR_C = 6, TR_R1 = 9, TR_R2 = 12, TR_MN = 15, TR_UV = 18, TR_SIZE = 24 };
+// RECTANGLE: R, raw A B C D, UV: ad = D-A, dc = C-D, nadc = |ad|*|dc|
+enum { RC_R = 0, RC_A = 14, RC_B = 17, RC_C = 20, RC_D = 23, RC_AD = 26, RC_DC = 29, RC_NADC = 32,
+       RC_SIZE = 33 };
+// RECTPRISM_V2: six face records, getNorm constants, face-0 UV block
+enum { PR_F = 0, PR_NBOT = 84, PR_NRIGHT = 87, PR_NFRONT = 90, PR_A = 93, PR_G = 96, PR_AD = 99,
+       PR_DC = 102, PR_NADC = 105, PR_D = 106, PR_SIZE = 109 };
+// CHECKERBOARD / CHECKERBOARD_HOLE: R, gn = normalized((B-A)x(C-A)) (edge test), raw A B C D,
+//   hole R, S, color1, color2, color, UV: ad, dc, nadc, miniu_dist, miniv_dist, bw
+enum { CK_R = 0, CK_GN = 14, CK_A = 17, CK_B = 20, CK_C = 23, CK_D = 26, CK_HOLE = 29, CK_S = 43,
+       CK_COL1 = 44, CK_COL2 = 47, CK_COL = 50, CK_AD = 53, CK_DC = 56, CK_NADC = 59, CK_MUD = 60,
+       CK_MVD = 61, CK_BW = 62, CK_SIZE = 63 };
+
+// per-render constants (kernel argument, < 4 KB)
+struct DParams {
+  int32_t xRes, yRes;
+  int32_t spp;            // sampled_n = int(sqrt(antialias_samples))^2 (cpp:1046,1061)
+  int32_t ppw;            // pixels per wave item (spp <= 64) ; 1 otherwise
+  int32_t chunks;         // ceil(spp/64)
+  int32_t max_depth, brdf_samples, blur_samples, frame_range;
+  int32_t frame;
+  int32_t frame_prism, frame_blur, frame_cloud;
+  int32_t reflect, nogloss, perlin_cloud;
+  int32_t n_nodes, n_lights, n_shapes;
+  int32_t n_cloud_steps;
+  uint32_t seed;
+  float aperture, focal_length, near_plane;
+  float l, r, t, b;
+  float refr_air, refr_glass, phong;
+  float move_per_frame, accel_t;
+  float saturation, cloudhoff;
+  float frame_f;          // float(frame) as passed to cloudColor
+  // tiles
+  int32_t x0, y0, x1, y1, tw, th, rank, world, layout, tiles_x;
+  int64_t n_owned_tiles;
+  int64_t n_items;
+  // camera
+  double eye[3], X[3], Y[3], Z[3];
+  double sky_m[3][4];     // rows 0..2 of mcam / new_mcam (cpp:1013-1021)
+  double default_col[3];
+  double sun[3];          // sundir.normalized() (cpp:152)
+  double sun_outer[3], sun_inner[3], sun_core[3], bluesky[3], redsky[3];
+};
+
+}  // namespace dtd

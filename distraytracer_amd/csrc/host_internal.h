@@ -1,0 +1,40 @@
+// host_internal.h — host-side pieces of libdt (not part of the C ABI).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "../../include/dt.h"
+#include "dt_math.h"
+#include "dt_scene_dev.h"
+
+namespace dth {
+
+struct FlatBVH {
+  std::vector<dtd::DNode> nodes;   // traversal order, skip links
+  std::vector<int32_t> leaf_idx;
+  std::vector<int32_t> depth;
+  std::vector<int32_t> n_children;
+};
+
+void shape_bounds(const dt_shape_desc& sh, dtm::V3& lb, dtm::V3& ub);
+void build_bvh(const dt_scene_desc& d, const dt_globals& g, FlatBVH& out);
+
+// device-layout scene produced from a descriptor (host_flatten.cpp)
+struct FlatScene {
+  FlatBVH bvh;
+  std::vector<dtd::DShapeHdr> hdr;
+  std::vector<double> geom;
+  std::vector<dtd::DMat> mat;
+  std::vector<dtd::DLight> lights;
+  std::vector<uint8_t> tex;
+};
+int flatten_scene(const dt_scene_desc& d, const dt_globals& g, FlatScene& out, std::string& err);
+
+// camera / params (host_flatten.cpp)
+int fill_params(const dt_globals& g, int frame, const dt_tiles* tiles, dtd::DParams& P, std::string& err);
+int fill_sky_params(const dt_globals& g, float frame, const dt_tiles* tiles, dtd::DParams& P, std::string& err);
+std::vector<float> cloud_z_steps(const dt_globals& g);
+
+void set_error(const std::string& e);
+
+}  // namespace dth
