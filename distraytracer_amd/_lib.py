@@ -81,7 +81,8 @@ class Stats(ctypes.Structure):
     _fields_ = [("pixels", c_uint64), ("samples", c_uint64), ("rays", c_uint64), ("shadow_rays", c_uint64),
                 ("sky_pixels", c_uint64), ("uv_out_of_range", c_uint64), ("glossy_exhausted", c_uint64),
                 ("spherelight_exhausted", c_uint64), ("prism_norm_fallback", c_uint64),
-                ("reflect_errors", c_uint64), ("nan_pixels", c_uint64), ("kernel_ms", c_double),
+                ("reflect_errors", c_uint64), ("nan_pixels", c_uint64), ("tex_fetches", c_uint64),
+                ("stack_overflows", c_uint64), ("kernel_ms", c_double),
                 ("trace_kernel_ms", c_double)]
 
     def as_dict(self):

@@ -41,7 +41,7 @@ struct HScene {
 };
 
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
-       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_N = 16 };
+       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_N = 16 };
 
 int fail(int code, const std::string& msg)
 {
@@ -99,6 +99,10 @@ struct dt_scene {
   unsigned long long* d_stats = nullptr;   // ST_N counters + queue word
   void* d_launch = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev_copy = nullptr;   // staging buffers may be rewritten once this has fired
+  uint8_t* h_launch = nullptr;    // pinned staging for the launch record
+  float* h_zs = nullptr;          // pinned staging for the cloud z sequence
+  bool copy_pending = false;
   bool timed = false;
   dtd::DParams last;
 };
@@ -186,7 +190,9 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
   }
   if (hipMalloc((void**)&s->d_stats, sizeof(unsigned long long) * (ST_N + 16)) != hipSuccess ||
       hipMalloc(&s->d_launch, dt_launch_size()) != hipSuccess || hipEventCreate(&s->ev0) != hipSuccess ||
-      hipEventCreate(&s->ev1) != hipSuccess) {
+      hipEventCreate(&s->ev1) != hipSuccess || hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc((void**)&s->h_launch, dt_launch_size(), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&s->h_zs, 2048 * sizeof(float), hipHostMallocDefault) != hipSuccess) {
     dt_scene_destroy(s);
     return fail(DT_E_NO_DEVICE, "device allocation failed");
   }
@@ -203,6 +209,9 @@ void dt_scene_destroy(dt_scene* s)
     if (b) (void)hipFree(b);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
+  if (s->ev_copy) (void)hipEventDestroy(s->ev_copy);
+  if (s->h_launch) (void)hipHostFree(s->h_launch);
+  if (s->h_zs) (void)hipHostFree(s->h_zs);
   delete s;
 }
 
@@ -266,14 +275,19 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
 static int enqueue_render(dt_scene* sc, const dtd::DParams& P, const std::vector<float>& zs, float* out_dev,
                           hipStream_t st)
 {
-  if (zs.size() > sc->zs_cap) {
+  // Fully asynchronous: the launch record and z table go through pinned staging that is
+  // only rewritten after the previous call's copies have executed (ev_copy); the device
+  // copies themselves are stream-ordered after any earlier kernel that reads them.
+  if (sc->copy_pending) HIPCHK(hipEventSynchronize(sc->ev_copy));
+  size_t nz = zs.size() < 2048 ? zs.size() : 2048;
+  if (nz > sc->zs_cap) {
+    if (sc->d_zs) HIPCHK(hipStreamSynchronize(st));
     if (sc->d_zs) (void)hipFree(sc->d_zs);
     sc->d_zs = nullptr;
-    sc->zs_cap = zs.size() + 64;
+    sc->zs_cap = 2048;
     HIPCHK(hipMalloc(&sc->d_zs, sc->zs_cap * sizeof(float)));
   }
-  if (!zs.empty()) HIPCHK(hipMemcpyAsync(sc->d_zs, zs.data(), zs.size() * sizeof(float), hipMemcpyHostToDevice, st));
-  std::vector<uint8_t> L(dt_launch_size(), 0);
+  if (nz) memcpy(sc->h_zs, zs.data(), nz * sizeof(float));
   HScene hs;
   hs.nodes = sc->d_nodes;
   hs.leaf_idx = (const int32_t*)sc->d_leaf;
@@ -285,9 +299,13 @@ static int enqueue_render(dt_scene* sc, const dtd::DParams& P, const std::vector
   hs.cloud_z = (const float*)sc->d_zs;
   hs.stats = sc->d_stats;
   hs.queue = sc->d_stats + ST_N;
-  memcpy(L.data() + dt_scene_struct_offset(), &hs, sizeof(hs));
-  memcpy(L.data() + dt_params_struct_offset(), &P, sizeof(P));
-  HIPCHK(hipMemcpyAsync(sc->d_launch, L.data(), L.size(), hipMemcpyHostToDevice, st));
+  memset(sc->h_launch, 0, dt_launch_size());
+  memcpy(sc->h_launch + dt_scene_struct_offset(), &hs, sizeof(hs));
+  memcpy(sc->h_launch + dt_params_struct_offset(), &P, sizeof(P));
+  if (nz) HIPCHK(hipMemcpyAsync(sc->d_zs, sc->h_zs, nz * sizeof(float), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(sc->d_launch, sc->h_launch, dt_launch_size(), hipMemcpyHostToDevice, st));
+  HIPCHK(hipEventRecord(sc->ev_copy, st));
+  sc->copy_pending = true;
   HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 16), st));
   static int resident = 0;
   if (!resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
@@ -298,8 +316,6 @@ static int enqueue_render(dt_scene* sc, const dtd::DParams& P, const std::vector
   HIPCHK(hipEventRecord(sc->ev1, st));
   sc->timed = true;
   sc->last = P;
-  // keep the host staging alive until the copy is done
-  HIPCHK(hipStreamSynchronize(st));
   return DT_OK;
 }
 
@@ -338,8 +354,10 @@ int dt_collect_stats(const dt_scene* sc_c, void* stream, dt_stats* stats)
   stats->glossy_exhausted = h[ST_GLOSSY];
   stats->spherelight_exhausted = h[ST_SPHL];
   stats->prism_norm_fallback = h[ST_PRISM];
-  stats->reflect_errors = h[ST_REFL] + h[ST_STACK];
+  stats->reflect_errors = h[ST_REFL];
   stats->nan_pixels = h[ST_NAN];
+  stats->tex_fetches = h[ST_TEX];
+  stats->stack_overflows = h[ST_STACK];
   if (sc->timed) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, sc->ev0, sc->ev1) == hipSuccess) {

@@ -37,7 +37,7 @@ using namespace dtd;
 #define DT_WAVE 64
 
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
-       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_N = 16 };
+       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_N = 16 };
 
 __constant__ uint32_t c_primes[10][3] = {
     {995615039u, 600173719u, 701464987u}, {831731269u, 162318869u, 136250887u},
@@ -938,7 +938,7 @@ __device__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t r
     e.a = ray0; e.b = org0; e.k = 1.0f; e.depth = P.max_depth; e.key = rootkey; e._pad = 1;  // root
     stack[sp++] = e;
   }
-  unsigned long long n_rays = 0, n_shadow = 0;
+  unsigned long long n_rays = 0, n_shadow = 0, n_tex = 0;
   while (true) {
     // pop FINISH entries (own-light contributions), then the next NODE
     bool have = false;
@@ -1135,6 +1135,7 @@ __device__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t r
                 if (uv_ind < 0) uv_ind = 0;
                 if (uv_ind >= M.tex_w * M.tex_h) uv_ind = M.tex_w * M.tex_h - 1;
                 const uint8_t* px = S.tex + M.tex_off + (int64_t)uv_ind * M.tex_ch;
+                n_tex++;
                 shape_color = v3(px[0] / 255.0, px[1] / 255.0, px[2] / 255.0);
               }
             }
@@ -1198,6 +1199,7 @@ __device__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t r
   }
   if (n_rays) atomicAdd(S.stats + ST_RAYS, n_rays);
   if (n_shadow) atomicAdd(S.stats + ST_SHADOW, n_shadow);
+  if (n_tex) atomicAdd(S.stats + ST_TEX, n_tex);
 }
 
 // =====================================================================================

@@ -213,6 +213,8 @@ typedef struct dt_stats {
   uint64_t prism_norm_fallback;   /* RectPrismV2::getNorm off-surface (geometry.cpp:895) */
   uint64_t reflect_errors;    /* refl.n <= 0 (cpp:631-638)                       */
   uint64_t nan_pixels;
+  uint64_t tex_fetches;       /* texel reads (algorithmic bytes) */
+  uint64_t stack_overflows;   /* DFS entries dropped (device stack limit); 0 when validated */
   double   kernel_ms;         /* device time of the render kernels (hipEvents, same stream) */
   double   trace_kernel_ms;   /* device time of the dominant (trace) kernel alone */
 } dt_stats;
