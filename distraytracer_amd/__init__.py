@@ -19,7 +19,7 @@ from ._lib import (DATA_DIR, DT_OUT_IMAGE, DT_OUT_SLAB, BVHNode, DTError, Global
 
 __all__ = ["Globals", "Tiles", "Stats", "DTError", "globals_default", "build_scene", "Scene",
            "render", "render_sky", "renderImage", "renderImageCloud", "write_ppm", "DATA_DIR",
-           "DT_OUT_IMAGE", "DT_OUT_SLAB", "slab_floats", "slab_floats_max", "unpack_slabs", "tiles"]
+           "DT_OUT_IMAGE", "DT_OUT_SLAB", "slab_floats", "slab_floats_max", "unpack_slabs", "tiles", "check", "lib"]
 
 
 def globals_default():

@@ -96,7 +96,7 @@ class BVHNode(ctypes.Structure):
 
 # every symbol include/dt.h declares (checked by tests/test_abi.py)
 EXPORTS = ["dt_abi_version", "dt_last_error", "dt_globals_default", "dt_scene_create", "dt_scene_destroy",
-           "dt_scene_bvh", "dt_slab_floats", "dt_slab_floats_max", "dt_render", "dt_render_async",
+           "dt_scene_bvh", "dt_bvh_build", "dt_slab_floats", "dt_slab_floats_max", "dt_render", "dt_render_async",
            "dt_collect_stats", "dt_render_sky", "dt_unpack_slabs", "dt_build_scene", "dt_scene_desc_free",
            "dt_write_ppm", "dt_mocap_bone_table"]
 
@@ -118,6 +118,8 @@ def _load():
         "dt_scene_create": (c_int32, [P(SceneDesc), P(Globals), P(ctypes.c_void_p)]),
         "dt_scene_destroy": (None, [ctypes.c_void_p]),
         "dt_scene_bvh": (c_int32, [ctypes.c_void_p, P(BVHNode), c_int32, P(c_int32), c_int32, P(c_int32),
+                                   P(c_int32)]),
+        "dt_bvh_build": (c_int32, [P(SceneDesc), P(Globals), P(BVHNode), c_int32, P(c_int32), c_int32, P(c_int32),
                                    P(c_int32)]),
         "dt_slab_floats": (c_int64, [P(Globals), P(Tiles)]),
         "dt_slab_floats_max": (c_int64, [P(Globals), P(Tiles)]),

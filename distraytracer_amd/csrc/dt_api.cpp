@@ -215,11 +215,9 @@ void dt_scene_destroy(dt_scene* s)
   delete s;
 }
 
-int dt_scene_bvh(const dt_scene* s, dt_bvh_node* nodes, int32_t cap, int32_t* indices, int32_t index_cap,
-                 int32_t* n_nodes, int32_t* n_indices)
+static int export_bvh(const FlatBVH& b, dt_bvh_node* nodes, int32_t cap, int32_t* indices, int32_t index_cap,
+                      int32_t* n_nodes, int32_t* n_indices)
 {
-  if (!s) return fail(DT_E_INVALID, "null scene");
-  const FlatBVH& b = s->flat.bvh;
   for (size_t i = 0; i < b.nodes.size() && (int32_t)i < cap; ++i) {
     const dtd::DNode& n = b.nodes[i];
     dt_bvh_node& o = nodes[i];
@@ -238,6 +236,23 @@ int dt_scene_bvh(const dt_scene* s, dt_bvh_node* nodes, int32_t cap, int32_t* in
   if (n_nodes) *n_nodes = (int32_t)b.nodes.size();
   if (n_indices) *n_indices = (int32_t)b.leaf_idx.size();
   return DT_OK;
+}
+
+int dt_scene_bvh(const dt_scene* s, dt_bvh_node* nodes, int32_t cap, int32_t* indices, int32_t index_cap,
+                 int32_t* n_nodes, int32_t* n_indices)
+{
+  if (!s) return fail(DT_E_INVALID, "null scene");
+  return export_bvh(s->flat.bvh, nodes, cap, indices, index_cap, n_nodes, n_indices);
+}
+
+int dt_bvh_build(const dt_scene_desc* desc, const dt_globals* g, dt_bvh_node* nodes, int32_t cap, int32_t* indices,
+                 int32_t index_cap, int32_t* n_nodes, int32_t* n_indices)
+{
+  if (!desc || !g) return fail(DT_E_INVALID, "null argument");
+  if (desc->n_shapes < 0 || (desc->n_shapes > 0 && !desc->shapes)) return fail(DT_E_INVALID, "invalid descriptor");
+  FlatBVH b;
+  build_bvh(*desc, *g, b);
+  return export_bvh(b, nodes, cap, indices, index_cap, n_nodes, n_indices);
 }
 
 int64_t dt_slab_floats(const dt_globals* g, const dt_tiles* tiles)

@@ -46,6 +46,21 @@ __constant__ uint32_t c_primes[10][3] = {
     {405493717u, 291031019u, 391950901u}, {458904767u, 676625681u, 424452397u},
     {531736441u, 939683957u, 810651871u}, {997169939u, 842027887u, 423882827u}};
 
+// Read-only scene arrays are accessed through the constant address space: with a wave-uniform
+// index (BVH walk, leaf shapes, lights) the compiler emits scalar s_load's into SGPRs
+// (scalar cache), with a per-lane index (hit-shape shading) ordinary vector loads.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DT_CAS __attribute__((address_space(4)))
+#else
+#define DT_CAS
+#endif
+template <class T>
+__device__ __forceinline__ const DT_CAS T* cas(const T* p)
+{
+  return (const DT_CAS T*)p;
+}
+typedef const DT_CAS double* GP;
+
 struct DScene {
   const DNode* nodes;
   const int32_t* leaf_idx;
@@ -257,10 +272,10 @@ struct Rng {
 // =====================================================================================
 // primitives (geometry.cpp), geometry from the precomputed pool
 // =====================================================================================
-__device__ __forceinline__ V3 G3(const double* __restrict__ g, int o) { return v3(g[o], g[o + 1], g[o + 2]); }
+__device__ __forceinline__ V3 G3(GP g, int o) { return v3(g[o], g[o + 1], g[o + 2]); }
 
 // Rectangle plane + quad bounds test (geometry.cpp:640-741 / 2292-2312): R record
-__device__ __forceinline__ bool rect_hit_R(const double* __restrict__ R, V3 ray, V3 start, float eps,
+__device__ __forceinline__ bool rect_hit_R(GP R, V3 ray, V3 start, float eps,
                                            float& t_out, float& ch1, float& ch2)
 {
   V3 A = G3(R, R_A), n = G3(R, R_N);
@@ -301,7 +316,7 @@ __device__ bool rect_hit_raw(V3 A, V3 B, V3 C, V3 D, V3 ray, V3 start, float eps
   return false;
 }
 
-__device__ __forceinline__ void shifted_rect(const double* __restrict__ g, float shift, V3& A, V3& B,
+__device__ __forceinline__ void shifted_rect(GP g, float shift, V3& A, V3& B,
                                              V3& C, V3& D)
 {
   A = G3(g, RC_A); B = G3(g, RC_B); C = G3(g, RC_C); D = G3(g, RC_D);
@@ -319,7 +334,7 @@ __device__ __forceinline__ bool quad_roots(float A, float B, float C, float& t0,
   return true;
 }
 
-__device__ __forceinline__ bool sphere_hit(const double* __restrict__ g, V3 ray, V3 start, float& t,
+__device__ __forceinline__ bool sphere_hit(GP g, V3 ray, V3 start, float& t,
                                            int& inside)
 {
   V3 sc = sub(start, G3(g, SP_C));
@@ -335,7 +350,7 @@ __device__ __forceinline__ bool sphere_hit(const double* __restrict__ g, V3 ray,
   return true;
 }
 
-__device__ __forceinline__ bool sphere_shadow(const double* __restrict__ g, V3 ray, V3 start, float t_max)
+__device__ __forceinline__ bool sphere_shadow(GP g, V3 ray, V3 start, float t_max)
 {
   const float eps = 1e-3f;
   V3 sc = sub(start, G3(g, SP_C));
@@ -347,7 +362,7 @@ __device__ __forceinline__ bool sphere_shadow(const double* __restrict__ g, V3 r
   return !((t0 <= eps || t0 >= t_max) && (t1 <= eps || t1 >= t_max));
 }
 
-__device__ __forceinline__ void cyl_coef(const double* __restrict__ g, V3 ray, V3 start, float& A,
+__device__ __forceinline__ void cyl_coef(GP g, V3 ray, V3 start, float& A,
                                          float& B, float& C)
 {
   V3 axis = G3(g, CY_AX);
@@ -359,13 +374,13 @@ __device__ __forceinline__ void cyl_coef(const double* __restrict__ g, V3 ray, V
   C = (float)(dot(cst, cst) - g[CY_R2]);
 }
 
-__device__ __forceinline__ bool cyl_in_caps(const double* __restrict__ g, V3 p)
+__device__ __forceinline__ bool cyl_in_caps(GP g, V3 p)
 {
   V3 axis = G3(g, CY_AX);
   return dot(axis, sub(p, G3(g, CY_C1))) > 0 && dot(axis, sub(p, G3(g, CY_C2))) < 0;
 }
 
-__device__ bool cyl_hit(const double* __restrict__ g, V3 ray, V3 start, float& t, int& inside)
+__device__ bool cyl_hit(GP g, V3 ray, V3 start, float& t, int& inside)
 {
   const float eps = 1e-3f;
   float A, B, C, t1, t2;
@@ -380,7 +395,7 @@ __device__ bool cyl_hit(const double* __restrict__ g, V3 ray, V3 start, float& t
   return false;
 }
 
-__device__ bool cyl_shadow(const double* __restrict__ g, V3 ray, V3 start, float t_max)
+__device__ bool cyl_shadow(GP g, V3 ray, V3 start, float t_max)
 {
   const float eps = 1e-3f;
   float A, B, C, t1, t2;
@@ -392,7 +407,7 @@ __device__ bool cyl_shadow(const double* __restrict__ g, V3 ray, V3 start, float
 }
 
 // Moller-Trumbore (geometry.cpp:488-586); returns 0 miss, else writes t_final
-__device__ __forceinline__ bool tri_core(const double* __restrict__ g, V3 ray, V3 start, float& t_final)
+__device__ __forceinline__ bool tri_core(GP g, V3 ray, V3 start, float& t_final)
 {
   V3 r1 = G3(g, TR_R1), r2 = G3(g, TR_R2);
   V3 h = cross(ray, r2);
@@ -425,7 +440,7 @@ __device__ bool segment_hit(V3 A, V3 B, V3 ray, V3 origin)
 }
 
 // GeoPrimitive::intersect. t only written when the reference writes it (Q16).
-__device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, const double* __restrict__ g,
+__device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, GP g,
                           V3 ray, V3 start, float shift, float& t, int& inside, V3& ccol, int& has_ccol)
 {
   has_ccol = 0;
@@ -510,7 +525,7 @@ __device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, co
 }
 
 // GeoPrimitive::intersectShadow
-__device__ bool shape_shadow(int type, uint32_t flags, const double* __restrict__ g, V3 ray, V3 start,
+__device__ bool shape_shadow(int type, uint32_t flags, GP g, V3 ray, V3 start,
                              float t_max, float shift)
 {
   float tt, a, b;
@@ -550,7 +565,7 @@ __device__ bool shape_shadow(int type, uint32_t flags, const double* __restrict_
 }
 
 // GeoPrimitive::getNorm (per-lane shape index)
-__device__ V3 shape_norm(int type, uint32_t flags, const double* __restrict__ g, V3 p, float shift,
+__device__ V3 shape_norm(int type, uint32_t flags, GP g, V3 p, float shift,
                          unsigned long long* st_prism)
 {
   switch (type) {
@@ -602,7 +617,7 @@ __device__ V3 shape_norm(int type, uint32_t flags, const double* __restrict__ g,
 }
 
 // GeoPrimitive::getUV (type 0/1/2)
-__device__ int shape_uv(int type, uint32_t flags, const double* __restrict__ g, V3 p, float shift,
+__device__ int shape_uv(int type, uint32_t flags, GP g, V3 p, float shift,
                         double& uo, double& vo)
 {
   switch (type) {
@@ -761,18 +776,18 @@ __device__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 r
   int i = 0;
   const int n_nodes = P.n_nodes;
   while (i < n_nodes) {
-    const DNode nd = S.nodes[i];
+    const DNode nd = cas(S.nodes)[i];
     bool act = resume <= i;
     bool hb = act && box_hit(nd, shift, ray, inv, org);
     if (nd.leaf) {
       if (__ballot(hb)) {
         for (int q = 0; q < nd.count; ++q) {
-          int sid = uni(S.leaf_idx[nd.first + q]);
-          DShapeHdr hd = S.hdr[sid];
+          int sid = uni(cas(S.leaf_idx)[nd.first + q]);
+          DShapeHdr hd = cas(S.hdr)[sid];
           if (hb) {
             int ins = 0, hc = 0;
             V3 cc;
-            if (shape_hit(S, sid, hd.type, hd.flags, S.geom + hd.off, ray, org, shift, t_dist, ins, cc, hc)) {
+            if (shape_hit(S, sid, hd.type, hd.flags, cas(S.geom) + hd.off, ray, org, shift, t_dist, ins, cc, hc)) {
               any = true;
               if (t_dist < h.t_min) {
                 h.shape = sid;
@@ -806,16 +821,16 @@ __device__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray
   int i = 0;
   const int n_nodes = P.n_nodes;
   while (i < n_nodes) {
-    const DNode nd = S.nodes[i];
+    const DNode nd = cas(S.nodes)[i];
     bool act = resume <= i;
     bool hb = act && box_hit(nd, shift, sray, inv, bstart);
     if (nd.leaf) {
       if (__ballot(hb)) {
         for (int q = 0; q < nd.count; ++q) {
-          int sid = uni(S.leaf_idx[nd.first + q]);
-          DShapeHdr hd = S.hdr[sid];
+          int sid = uni(cas(S.leaf_idx)[nd.first + q]);
+          DShapeHdr hd = cas(S.hdr)[sid];
           if (hb && !occl && sid != skip_shape) {
-            if (shape_shadow(hd.type, hd.flags, S.geom + hd.off, sn, sstart, t_max, shift)) occl = true;
+            if (shape_shadow(hd.type, hd.flags, cas(S.geom) + hd.off, sn, sstart, t_max, shift)) occl = true;
           }
         }
       }
@@ -927,7 +942,7 @@ __device__ __forceinline__ float schlick_complex(float cos_theta, double r0, dou
 
 // One full rayColor tree for the lanes with `active`. Appends to out.color in the
 // reference's accumulation order.
-__device__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t rootkey, float shift,
+__device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t rootkey, float shift,
                          PassOut& out, Entry* stack)
 {
   const DScene& S = *c.S;
@@ -947,7 +962,7 @@ __device__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t r
       e = stack[--sp];
       if (e.depth < 0) {
         out.color = add(out.color, e.a);
-      } else {
+      } else if (e.depth > 0) {
         have = true;
         break;
       }
@@ -975,7 +990,7 @@ __device__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t r
     V3 own = v3(0, 0, 0);
     if (any) {
       hd = S.hdr[sid];
-      const double* g = S.geom + hd.off;
+      GP g = cas(S.geom) + hd.off;
       const DMat& M = S.mat[sid];
       isectP = add(eye, mul(h.t_min, ray));
       normal = shape_norm(hd.type, hd.flags, g, isectP, shift, S.stats + ST_PRISM);
@@ -992,80 +1007,88 @@ __device__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t r
         const float eps = 1e-3f;
         const bool glossy = (M.flags & DT_F_GLOSSY) != 0;
         float k_refl = 1, k_refr = 1;
-        // children are pushed in reverse call order after being generated in call order
-        Entry kids[8];
-        int nk = 0;
-        if (M.material == DT_MAT_GLASS) {
-          float cos_theta = (float)dot(normal, neg(in));
-          float sin_theta = (float)sqrt(1 - pow((double)cos_theta, 2.0));
-          float r1 = h.inside ? P.refr_glass : P.refr_air, r2 = h.inside ? P.refr_air : P.refr_glass;
-          float chk = (float)(1 - pow((double)(r1 / r2), 2.0) * (1 - pow(dot(in, normal), 2.0)));
-          if (chk >= 0) {
-            float a = r1 / r2 * sin_theta;
-            float b = 1 / sin_theta;
-            float sq = sqrtf(chk);
-            V3 outr = sub(mul(a, mul(b, add(in, mul(cos_theta, normal)))), mul(sq, normal));
-            V3 adj_org = add(isectP, mul(eps, in));
-            float cos_phi = (float)sqrt(1 - pow((double)(P.refr_glass / P.refr_air), 2.0) *
-                                                (1 - pow(dot(in, normal), 2.0)));
-            float rp = (P.refr_glass * cos_theta - P.refr_air * cos_phi) /
-                       (P.refr_glass * cos_theta + P.refr_air * cos_phi);
-            float rs = (P.refr_air * cos_theta - P.refr_glass * cos_phi) /
-                       (P.refr_air * cos_theta + P.refr_glass * cos_phi);
-            k_refl = (float)(0.5 * (pow((double)rp, 2.0) + pow((double)rs, 2.0)));
-            k_refr = 1 - k_refl;
-            Entry ch; ch.a = outr; ch.b = adj_org; ch.k = k_refr * k; ch.depth = depth - 1;
-            ch.key = child_key(node, 0); ch._pad = 0;
-            kids[nk++] = ch;
-          }
-        }
-        V3 refl_ray = sub(in, mul(2 * dot(normal, in), normal));
-        if (dot(refl_ray, normal) <= 0) {
-          atomicAdd(S.stats + ST_REFL, 1ull);
-        } else if (dot(refl_ray, normal) > eps) {
-          if (glossy && !P.nogloss) {
-            V3 A, B, C, D, wv, lv;
-            glossy_rect(refl_ray, isectP, 2.0f, A, B, C, D, wv, lv);
-            V3 wa = wv, la = lv;
-            if (dot(wv, normal) <= 0) wa = neg(wa);
-            if (dot(lv, normal) <= 0) la = neg(la);
-            // squeeze (cpp:680-695); bounded so a degenerate normal cannot hang the GPU
-            for (int it = 0; it < 100000 && dot(sub(A, isectP), normal) <= 0; ++it) A = add(add(A, mul(0.1, wa)), mul(0.1, la));
-            for (int it = 0; it < 100000 && dot(sub(B, isectP), normal) <= 0; ++it) B = add(add(B, mul(0.1, wa)), mul(0.1, la));
-            for (int it = 0; it < 100000 && dot(sub(C, isectP), normal) <= 0; ++it) C = add(add(C, mul(0.1, wa)), mul(0.1, la));
-            for (int it = 0; it < 100000 && dot(sub(D, isectP), normal) <= 0; ++it) D = add(add(D, mul(0.1, wa)), mul(0.1, la));
-            for (int i = 0; i < P.brdf_samples && nk < 8; i++) {
-              int attempt = 0;
-              double u0, u1;
-              c.rng.draw(node, P_GLOSSY, ((uint32_t)i << 8) | (uint32_t)attempt, u0, u1);
-              V3 sample_refl = sub(rect_sample(A, B, D, u0, u1), isectP);
-              int sample_limit = 10;
-              bool exhausted = false;
-              while (dot(sample_refl, normal) <= 0) {
-                if (sample_limit < 0) { exhausted = true; break; }
-                float multiplier = (float)pow(2.0, (double)(11 - sample_limit));
-                glossy_rect(refl_ray, isectP, multiplier, A, B, C, D, wv, lv);
-                attempt++;
-                c.rng.draw(node, P_GLOSSY, ((uint32_t)i << 8) | (uint32_t)attempt, u0, u1);
-                sample_refl = sub(rect_sample(A, B, D, u0, u1), isectP);
-                sample_limit--;
-              }
-              if (exhausted) { atomicAdd(S.stats + ST_GLOSSY, 1ull); continue; }
-              Entry ch; ch.a = sample_refl; ch.b = add(isectP, mul(eps, sample_refl));
-              ch.k = k_refl * k / P.brdf_samples; ch.depth = depth - 1; ch.key = child_key(node, 2 + i);
-              ch._pad = 0;
-              kids[nk++] = ch;
-            }
-          } else {
-            Entry ch; ch.a = refl_ray; ch.b = add(isectP, mul(eps, refl_ray)); ch.k = k_refl * k;
-            ch.depth = depth - 1; ch.key = child_key(node, 1); ch._pad = 0;
-            kids[nk++] = ch;
-          }
-        }
+        // Children are written straight into their stack slots in reverse call order, so the
+        // reference's call order comes out of the LIFO: [base, base+nref) reflection children
+        // (glossy sample nref-1 .. 0, or the mirror ray), base+nref the refraction child
+        // (glass, called first in cpp:592-626). A glossy sample that exhausts its resamples
+        // leaves a depth-0 entry, which pops as a no-op (a depth-0 rayColor returns at once).
+        // At depth 1 the children would return immediately: none are generated.
         if (depth - 1 > 0) {
-          for (int q = nk - 1; q >= 0; --q) {
-            if (sp < DT_STACK_MAX) stack[sp++] = kids[q];
-            else atomicAdd(S.stats + ST_STACK, 1ull);
+          V3 refl_ray = sub(in, mul(2 * dot(normal, in), normal));
+          const double rn = dot(refl_ray, normal);
+          int nref = 0;
+          if (rn <= 0) atomicAdd(S.stats + ST_REFL, 1ull);
+          else if (rn > eps) nref = (glossy && !P.nogloss) ? P.brdf_samples : 1;
+          const bool glass = M.material == DT_MAT_GLASS;
+          const int base = sp;
+          if (base + nref + (glass ? 1 : 0) > DT_STACK_MAX) {
+            atomicAdd(S.stats + ST_STACK, 1ull);
+            nref = 0;
+          } else {
+            sp = base + nref;
+            if (glass) {
+              float cos_theta = (float)dot(normal, neg(in));
+              float sin_theta = (float)sqrt(1 - pow((double)cos_theta, 2.0));
+              float r1 = h.inside ? P.refr_glass : P.refr_air, r2 = h.inside ? P.refr_air : P.refr_glass;
+              float chk = (float)(1 - pow((double)(r1 / r2), 2.0) * (1 - pow(dot(in, normal), 2.0)));
+              if (chk >= 0) {
+                float a = r1 / r2 * sin_theta;
+                float b = 1 / sin_theta;
+                float sq = sqrtf(chk);
+                V3 outr = sub(mul(a, mul(b, add(in, mul(cos_theta, normal)))), mul(sq, normal));
+                V3 adj_org = add(isectP, mul(eps, in));
+                float cos_phi = (float)sqrt(1 - pow((double)(P.refr_glass / P.refr_air), 2.0) *
+                                                    (1 - pow(dot(in, normal), 2.0)));
+                float rp = (P.refr_glass * cos_theta - P.refr_air * cos_phi) /
+                           (P.refr_glass * cos_theta + P.refr_air * cos_phi);
+                float rs = (P.refr_air * cos_theta - P.refr_glass * cos_phi) /
+                           (P.refr_air * cos_theta + P.refr_glass * cos_phi);
+                k_refl = (float)(0.5 * (pow((double)rp, 2.0) + pow((double)rs, 2.0)));
+                k_refr = 1 - k_refl;
+                Entry ch; ch.a = outr; ch.b = adj_org; ch.k = k_refr * k; ch.depth = depth - 1;
+                ch.key = child_key(node, 0); ch._pad = 0;
+                stack[sp++] = ch;
+              }
+            }
+            if (nref > 0 && glossy && !P.nogloss) {
+              V3 A, B, C, D, wv, lv;
+              glossy_rect(refl_ray, isectP, 2.0f, A, B, C, D, wv, lv);
+              V3 wa = wv, la = lv;
+              if (dot(wv, normal) <= 0) wa = neg(wa);
+              if (dot(lv, normal) <= 0) la = neg(la);
+              // squeeze (cpp:680-695); bounded so a degenerate normal cannot hang the GPU
+              for (int it = 0; it < 100000 && dot(sub(A, isectP), normal) <= 0; ++it) A = add(add(A, mul(0.1, wa)), mul(0.1, la));
+              for (int it = 0; it < 100000 && dot(sub(B, isectP), normal) <= 0; ++it) B = add(add(B, mul(0.1, wa)), mul(0.1, la));
+              for (int it = 0; it < 100000 && dot(sub(C, isectP), normal) <= 0; ++it) C = add(add(C, mul(0.1, wa)), mul(0.1, la));
+              for (int it = 0; it < 100000 && dot(sub(D, isectP), normal) <= 0; ++it) D = add(add(D, mul(0.1, wa)), mul(0.1, la));
+              const float kg = k_refl * k / P.brdf_samples;
+              for (int i = 0; i < nref; i++) {
+                int attempt = 0;
+                double u0, u1;
+                c.rng.draw(node, P_GLOSSY, ((uint32_t)i << 8) | (uint32_t)attempt, u0, u1);
+                V3 sample_refl = sub(rect_sample(A, B, D, u0, u1), isectP);
+                int sample_limit = 10;
+                bool exhausted = false;
+                while (dot(sample_refl, normal) <= 0) {
+                  if (sample_limit < 0) { exhausted = true; break; }
+                  float multiplier = (float)pow(2.0, (double)(11 - sample_limit));
+                  glossy_rect(refl_ray, isectP, multiplier, A, B, C, D, wv, lv);
+                  attempt++;
+                  c.rng.draw(node, P_GLOSSY, ((uint32_t)i << 8) | (uint32_t)attempt, u0, u1);
+                  sample_refl = sub(rect_sample(A, B, D, u0, u1), isectP);
+                  sample_limit--;
+                }
+                if (exhausted) atomicAdd(S.stats + ST_GLOSSY, 1ull);
+                Entry ch; ch.a = sample_refl; ch.b = add(isectP, mul(eps, sample_refl));
+                ch.k = kg; ch.depth = exhausted ? 0 : depth - 1; ch.key = child_key(node, 2 + i);
+                ch._pad = 0;
+                stack[base + nref - 1 - i] = ch;
+              }
+            } else if (nref > 0) {
+              Entry ch; ch.a = refl_ray; ch.b = add(isectP, mul(eps, refl_ray)); ch.k = k_refl * k;
+              ch.depth = depth - 1; ch.key = child_key(node, 1); ch._pad = 0;
+              stack[base] = ch;
+            }
           }
         }
       }
@@ -1098,7 +1121,7 @@ __device__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t r
       bool aborted = false;
       V3 tmp_color = v3(0, 0, 0);
       for (int li = 0; li < P.n_lights; ++li) {
-        const DLight L = S.lights[li];
+        const DLight L = cas(S.lights)[li];
         bool lane = shade && !aborted;
         V3 sray = v3(1, 0, 0);
         float t_max = 0;
@@ -1113,7 +1136,7 @@ __device__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t r
                              t_max, L.shape_index, shift);
         if (lane && !occl) {
           const DMat& M = *Mp;
-          const double* g = S.geom + hd.off;
+          GP g = cas(S.geom) + hd.off;
           V3 lc = v3a(L.color);
           V3 r = normalized(add(mul(-1, sray), mul(2 * dot(normal, sray), normal)));
           bool skip_rest = false;
@@ -1291,21 +1314,22 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       V3 focalPoint = add(eye, mul(P.focal_length, rayDir));
       V3 ray0 = sub(focalPoint, eye_sample);
 
-      PassOut po;
-      po.color = v3(0, 0, 0);
-      po.hit = false;
-      po.in_motion = false;
-      run_pass(c, valid, ray0, eye_sample, root_key(0), 0.0f, po, stack);
-      V3 tmp_color = po.color;
-      const bool need_blur = valid && po.hit && po.in_motion;
-      if (__ballot(need_blur)) {   // motion blur re-traces (cpp:1095-1210)
-        for (int m = 0; m < P.blur_samples; ++m) {
-          float val = 0.0f;
-          if (need_blur) {
+      // pass 0: the sample's rayColor tree; passes 1..blur_samples: motion-blur re-traces for
+      // samples whose last hit was a moving shape (cpp:1095-1210). One call site so the DFS is
+      // inlined once.
+      V3 tmp_color = v3(0, 0, 0);
+      bool hit0 = false, need_blur = false;
+      for (int pass = 0; pass <= P.blur_samples; ++pass) {
+        bool act = valid;
+        float val = 0.0f;
+        if (pass > 0) {
+          if (!__ballot(need_blur)) break;
+          act = need_blur;
+          if (act) {
             double u0, u1;
-            c.rng.draw(0, P_BLUR, (uint32_t)m, u0, u1);
+            c.rng.draw(0, P_BLUR, (uint32_t)(pass - 1), u0, u1);
             float frame_sample = (float)((float)P.frame + u0 * P.frame_range);
-            if (P.frame >= P.frame_prism) {
+            if (P.frame >= P.frame_prism) {   // below frame_prism the reference's val is unset (Q19): 0
               if (P.frame >= P.frame_blur)
                 val = (float)(P.move_per_frame * (frame_sample - P.frame) +
                               P.accel_t * pow((double)(frame_sample - P.frame), 3.0));
@@ -1313,16 +1337,22 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
                 val = P.move_per_frame * (frame_sample - P.frame);
             }
           }
-          PassOut pm;
-          pm.color = v3(0, 0, 0);
-          pm.hit = true;
-          pm.in_motion = false;
-          run_pass(c, need_blur, ray0, eye_sample, root_key(m + 1), val, pm, stack);
-          if (need_blur) tmp_color = add(tmp_color, pm.color);
         }
-        if (need_blur) tmp_color = divs(tmp_color, P.blur_samples + 1);
+        PassOut po;
+        po.color = v3(0, 0, 0);
+        po.hit = pass > 0;
+        po.in_motion = false;
+        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack);
+        if (pass == 0) {
+          tmp_color = po.color;
+          hit0 = po.hit;
+          need_blur = valid && po.hit && po.in_motion;
+        } else if (need_blur) {
+          tmp_color = add(tmp_color, po.color);
+        }
       }
-      const bool miss = valid && !po.hit;
+      if (need_blur) tmp_color = divs(tmp_color, P.blur_samples + 1);
+      const bool miss = valid && !hit0;
       // sky for missing samples: computed once per pixel by the whole wave
       if (P.perlin_cloud) {
         for (int jj = 0; jj < group; ++jj) {

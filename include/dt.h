@@ -242,6 +242,11 @@ typedef struct dt_bvh_node {
 int  dt_scene_bvh(const dt_scene* s, dt_bvh_node* nodes, int32_t cap,
                   int32_t* indices, int32_t index_cap, int32_t* n_nodes, int32_t* n_indices);
 
+/* generateBVH (helpers.h:381-472) alone, on the host, no device needed: same export format
+ * as dt_scene_bvh. */
+int  dt_bvh_build(const dt_scene_desc* desc, const dt_globals* g, dt_bvh_node* nodes, int32_t cap,
+                  int32_t* indices, int32_t index_cap, int32_t* n_nodes, int32_t* n_indices);
+
 /* number of floats a DT_OUT_SLAB output needs for (g, tiles) */
 int64_t dt_slab_floats(const dt_globals* g, const dt_tiles* tiles);
 int64_t dt_slab_floats_max(const dt_globals* g, const dt_tiles* tiles); /* max over ranks */

