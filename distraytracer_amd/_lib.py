@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdt.so")
+LIB_PATH = os.environ.get("DT_LIB") or os.path.join(_HERE, "libdt.so")   # DT_LIB: A/B builds
 REPO_ROOT = os.path.dirname(_HERE)
 DATA_DIR = os.path.join(REPO_ROOT, "data")
 

@@ -863,6 +863,12 @@ struct PassOut {
   bool in_motion;
 };
 
+// per-lane event counters, kept in registers for the whole persistent loop and reduced
+// across the wave once at kernel exit (same-address atomics per lane serialise at L2)
+struct Counters {
+  uint32_t rays, shadow, tex;
+};
+
 struct Ctx {
   const DScene* S;
   const DParams* P;
@@ -943,7 +949,7 @@ __device__ __forceinline__ float schlick_complex(float cos_theta, double r0, dou
 // One full rayColor tree for the lanes with `active`. Appends to out.color in the
 // reference's accumulation order.
 __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t rootkey, float shift,
-                         PassOut& out, Entry* stack)
+                         PassOut& out, Entry* stack, Counters& cnt)
 {
   const DScene& S = *c.S;
   const DParams& P = *c.P;
@@ -953,7 +959,6 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     e.a = ray0; e.b = org0; e.k = 1.0f; e.depth = P.max_depth; e.key = rootkey; e._pad = 1;  // root
     stack[sp++] = e;
   }
-  unsigned long long n_rays = 0, n_shadow = 0, n_tex = 0;
   while (true) {
     // pop FINISH entries (own-light contributions), then the next NODE
     bool have = false;
@@ -973,7 +978,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     const float k = e.k;
     const uint32_t node = e.key;
     const bool is_root = have && e._pad == 1;
-    if (have) { out.in_motion = false; n_rays++; }   // cpp:519
+    if (have) { out.in_motion = false; cnt.rays++; }   // cpp:519
 
     HitRec h;
     bool any = closest_hit(S, P, have, ray, eye, shift, h);
@@ -1130,7 +1135,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL);
           t_max = (float)norm(sray);
           sn = normalized(sray);
-          n_shadow++;
+          cnt.shadow++;
         }
         bool occl = occluded(S, P, lane, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
                              t_max, L.shape_index, shift);
@@ -1158,7 +1163,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
                 if (uv_ind < 0) uv_ind = 0;
                 if (uv_ind >= M.tex_w * M.tex_h) uv_ind = M.tex_w * M.tex_h - 1;
                 const uint8_t* px = S.tex + M.tex_off + (int64_t)uv_ind * M.tex_ch;
-                n_tex++;
+                cnt.tex++;
                 shape_color = v3(px[0] / 255.0, px[1] / 255.0, px[2] / 255.0);
               }
             }
@@ -1220,9 +1225,14 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       stack[fin_slot] = f;
     }
   }
-  if (n_rays) atomicAdd(S.stats + ST_RAYS, n_rays);
-  if (n_shadow) atomicAdd(S.stats + ST_SHADOW, n_shadow);
-  if (n_tex) atomicAdd(S.stats + ST_TEX, n_tex);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(uint32_t v)
+{
+  unsigned long long x = v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
 }
 
 // =====================================================================================
@@ -1256,7 +1266,10 @@ struct DLaunch {
   DParams P;
 };
 
-extern "C" __global__ void __launch_bounds__(64)
+#ifndef DT_TRACE_MIN_WAVES
+#define DT_TRACE_MIN_WAVES 1
+#endif
+extern "C" __global__ void __launch_bounds__(64, DT_TRACE_MIN_WAVES)
 dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
 {
   const DScene& S = Lp->S;
@@ -1273,6 +1286,8 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   c.rng.k0 = P.seed;
   c.rng.k1 = (uint32_t)P.frame;
   unsigned long long sky_px = 0;
+  Counters cnt;
+  cnt.rays = 0; cnt.shadow = 0; cnt.tex = 0;
 
   while (true) {
     if (lane == 0) item_s = atomicAdd(S.queue, 1ull);
@@ -1342,7 +1357,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         po.color = v3(0, 0, 0);
         po.hit = pass > 0;
         po.in_motion = false;
-        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack);
+        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt);
         if (pass == 0) {
           tmp_color = po.color;
           hit0 = po.hit;
@@ -1403,7 +1418,15 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       }
     }
   }
-  if (lane == 0 && sky_px) atomicAdd(S.stats + ST_SKY, sky_px);
+  {
+    unsigned long long r = wave_sum(cnt.rays), sh = wave_sum(cnt.shadow), tx = wave_sum(cnt.tex);
+    if (lane == 0) {
+      if (sky_px) atomicAdd(S.stats + ST_SKY, sky_px);
+      atomicAdd(S.stats + ST_RAYS, r);
+      atomicAdd(S.stats + ST_SHADOW, sh);
+      atomicAdd(S.stats + ST_TEX, tx);
+    }
+  }
 }
 
 // renderImageCloud (cpp:1224-1279): one pixel per lane
