@@ -82,7 +82,8 @@ class Stats(ctypes.Structure):
                 ("sky_pixels", c_uint64), ("uv_out_of_range", c_uint64), ("glossy_exhausted", c_uint64),
                 ("spherelight_exhausted", c_uint64), ("prism_norm_fallback", c_uint64),
                 ("reflect_errors", c_uint64), ("nan_pixels", c_uint64), ("tex_fetches", c_uint64),
-                ("stack_overflows", c_uint64), ("kernel_ms", c_double),
+                ("stack_overflows", c_uint64), ("box_tests", c_uint64), ("prim_tests", c_uint64),
+                ("wave_node_visits", c_uint64), ("kernel_ms", c_double),
                 ("trace_kernel_ms", c_double)]
 
     def as_dict(self):

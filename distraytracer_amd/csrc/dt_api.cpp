@@ -41,7 +41,7 @@ struct HScene {
 };
 
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
-       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_N = 16 };
+       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15, ST_N = 16 };
 
 int fail(int code, const std::string& msg)
 {
@@ -373,6 +373,9 @@ int dt_collect_stats(const dt_scene* sc_c, void* stream, dt_stats* stats)
   stats->nan_pixels = h[ST_NAN];
   stats->tex_fetches = h[ST_TEX];
   stats->stack_overflows = h[ST_STACK];
+  stats->box_tests = h[ST_BOX];
+  stats->prim_tests = h[ST_PRIM];
+  stats->wave_node_visits = h[ST_WNODES];
   if (sc->timed) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, sc->ev0, sc->ev1) == hipSuccess) {

@@ -37,7 +37,7 @@ using namespace dtd;
 #define DT_WAVE 64
 
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
-       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_N = 16 };
+       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15, ST_N = 16 };
 
 __constant__ uint32_t c_primes[10][3] = {
     {995615039u, 600173719u, 701464987u}, {831731269u, 162318869u, 136250887u},
@@ -705,54 +705,66 @@ __device__ int shape_uv(int type, uint32_t flags, GP g, V3 p, float shift,
 // =====================================================================================
 // BVH: wave-uniform stackless traversal (geometry.cpp:2657-2740 box test)
 // =====================================================================================
-__device__ __forceinline__ bool box_hit(const DNode& b, float bump, V3 ray, V3 inv, V3 st)
+// Per-ray constants of the slab test, computed once per traversal.
+struct RayBox {
+  V3 inv;                      // ray.cwiseInverse()
+  bool nx, ny, nz;             // ray[a] < 0
+  bool ix, iy, iz;             // isinf(inv[a])
+};
+
+__device__ __forceinline__ RayBox make_raybox(V3 ray)
+{
+  RayBox r;
+  r.inv = v3(1.0 / ray.x, 1.0 / ray.y, 1.0 / ray.z);
+  r.nx = ray.x < 0; r.ny = ray.y < 0; r.nz = ray.z < 0;
+  r.ix = isinf(r.inv.x); r.iy = isinf(r.inv.y); r.iz = isinf(r.inv.z);
+  return r;
+}
+
+// BoundingVolume::intersect (geometry.cpp:2657-2740), branch-free: every early `return false`
+// of the reference becomes a cleared `ok`, every conditional assignment a select, so a wave
+// evaluates one straight-line sequence per node with no exec-mask traffic.
+__device__ __forceinline__ bool box_hit(const DNode& b, float bump, const RayBox& r, V3 st)
 {
   double lb1 = b.lb[1], ub1 = b.ub[1];
   if (b.leaf && bump != 0.0f) { lb1 = lb1 - bump; ub1 = ub1 + bump; }   // bumpBVH (helpers.h:530)
-  float tmin, tmax;
-  if (isinf(inv.x)) {
-    if (!(st.x >= b.lb[0] && st.x <= b.ub[0])) return false;
-    tmin = FLT_MIN; tmax = FLT_MAX;
-  } else if (ray.x < 0) {
-    tmin = (float)((b.ub[0] - st.x) * inv.x);
-    tmax = (float)((b.lb[0] - st.x) * inv.x);
-  } else {
-    tmin = (float)((b.lb[0] - st.x) * inv.x);
-    tmax = (float)((b.ub[0] - st.x) * inv.x);
+  bool ok;
+  float tmin, tmax, tymin, tymax, tzmin, tzmax;
+  {
+    double lo = r.nx ? b.ub[0] : b.lb[0], hi = r.nx ? b.lb[0] : b.ub[0];
+    float a = (float)((lo - st.x) * r.inv.x), c = (float)((hi - st.x) * r.inv.x);
+    bool in = (st.x >= b.lb[0]) & (st.x <= b.ub[0]);
+    tmin = r.ix ? FLT_MIN : a;
+    tmax = r.ix ? FLT_MAX : c;
+    ok = r.ix ? in : true;
   }
-  float tymin, tymax;
-  if (isinf(inv.y)) {
-    if (!(st.y >= lb1 && st.y <= ub1)) return false;
-    tymin = FLT_MIN; tymax = FLT_MAX;
-  } else if (ray.y < 0) {
-    tymin = (float)((ub1 - st.y) * inv.y);
-    tymax = (float)((lb1 - st.y) * inv.y);
-  } else {
-    tymin = (float)((lb1 - st.y) * inv.y);
-    tymax = (float)((ub1 - st.y) * inv.y);
+  {
+    double lo = r.ny ? ub1 : lb1, hi = r.ny ? lb1 : ub1;
+    float a = (float)((lo - st.y) * r.inv.y), c = (float)((hi - st.y) * r.inv.y);
+    bool in = (st.y >= lb1) & (st.y <= ub1);
+    tymin = r.iy ? FLT_MIN : a;
+    tymax = r.iy ? FLT_MAX : c;
+    ok = ok & (r.iy ? in : true);
   }
-  if (tmin > tymax || tymin > tmax) return false;
-  if (tymin > tmin) tmin = tymin;
-  if (tymax < tmax) tmax = tymax;
-  float tzmin, tzmax;
-  if (isinf(inv.z)) {
-    if (!(st.z >= b.lb[2] && st.z <= b.ub[2])) return false;
-    tzmin = FLT_MIN; tzmax = FLT_MAX;
-  } else if (ray.z < 0) {
-    tzmin = (float)((b.ub[2] - st.z) * inv.z);
-    tzmax = (float)((b.lb[2] - st.z) * inv.z);
-  } else {
-    tzmin = (float)((b.lb[2] - st.z) * inv.z);
-    tzmax = (float)((b.ub[2] - st.z) * inv.z);
+  ok = ok & !((tmin > tymax) | (tymin > tmax));
+  tmin = (tymin > tmin) ? tymin : tmin;
+  tmax = (tymax < tmax) ? tymax : tmax;
+  {
+    double lo = r.nz ? b.ub[2] : b.lb[2], hi = r.nz ? b.lb[2] : b.ub[2];
+    float a = (float)((lo - st.z) * r.inv.z), c = (float)((hi - st.z) * r.inv.z);
+    bool in = (st.z >= b.lb[2]) & (st.z <= b.ub[2]);
+    tzmin = r.iz ? FLT_MIN : a;
+    tzmax = r.iz ? FLT_MAX : c;
+    ok = ok & (r.iz ? in : true);
   }
-  if (tmin > tzmax || tzmin > tmax) return false;
-  if (tzmin > tmin) tmin = tzmin;
-  if (tzmax < tmax) tmax = tzmax;
-  return tmax > 0;
+  ok = ok & !((tmin > tzmax) | (tzmin > tmax));
+  tmax = (tzmax < tmax) ? tzmax : tmax;
+  return ok & (tmax > 0);
 }
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+struct Counters;
 struct HitRec {
   float t_min;
   int shape;
@@ -762,10 +774,11 @@ struct HitRec {
 };
 
 // closest hit over the lanes with `active` (cpp:491-538)
-__device__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 ray, V3 org, float shift,
-                            HitRec& h)
+template <class CNT>
+__device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 ray, V3 org, float shift,
+                                            HitRec& h, CNT& cnt)
 {
-  V3 inv = v3(1.0 / ray.x, 1.0 / ray.y, 1.0 / ray.z);
+  const RayBox rb = make_raybox(ray);
   int resume = active ? 0 : 0x7fffffff;
   float t_dist = FLT_MAX;
   bool any = false;
@@ -778,13 +791,16 @@ __device__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 r
   while (i < n_nodes) {
     const DNode nd = cas(S.nodes)[i];
     bool act = resume <= i;
-    bool hb = act && box_hit(nd, shift, ray, inv, org);
+    bool hb = act && box_hit(nd, shift, rb, org);
+    cnt.wnodes++;
+    cnt.box += act;
     if (nd.leaf) {
       if (__ballot(hb)) {
         for (int q = 0; q < nd.count; ++q) {
           int sid = uni(cas(S.leaf_idx)[nd.first + q]);
           DShapeHdr hd = cas(S.hdr)[sid];
           if (hb) {
+            cnt.prim++;
             int ins = 0, hc = 0;
             V3 cc;
             if (shape_hit(S, sid, hd.type, hd.flags, cas(S.geom) + hd.off, ray, org, shift, t_dist, ins, cc, hc)) {
@@ -812,10 +828,11 @@ __device__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 r
 
 // any-hit shadow test (cpp:806-855): box test with sray from isectP+sray*1e-3, shape test
 // with normalized sray from isectP+sn*1e-3, skipping the light's own shape.
-__device__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
-                         V3 sstart, float t_max, int skip_shape, float shift)
+template <class CNT>
+__device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
+                                         V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
 {
-  V3 inv = v3(1.0 / sray.x, 1.0 / sray.y, 1.0 / sray.z);
+  const RayBox rb = make_raybox(sray);
   int resume = active ? 0 : 0x7fffffff;
   bool occl = false;
   int i = 0;
@@ -823,13 +840,16 @@ __device__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray
   while (i < n_nodes) {
     const DNode nd = cas(S.nodes)[i];
     bool act = resume <= i;
-    bool hb = act && box_hit(nd, shift, sray, inv, bstart);
+    bool hb = act && box_hit(nd, shift, rb, bstart);
+    cnt.wnodes++;
+    cnt.box += act;
     if (nd.leaf) {
       if (__ballot(hb)) {
         for (int q = 0; q < nd.count; ++q) {
           int sid = uni(cas(S.leaf_idx)[nd.first + q]);
           DShapeHdr hd = cas(S.hdr)[sid];
           if (hb && !occl && sid != skip_shape) {
+            cnt.prim++;
             if (shape_shadow(hd.type, hd.flags, cas(S.geom) + hd.off, sn, sstart, t_max, shift)) occl = true;
           }
         }
@@ -866,7 +886,7 @@ struct PassOut {
 // per-lane event counters, kept in registers for the whole persistent loop and reduced
 // across the wave once at kernel exit (same-address atomics per lane serialise at L2)
 struct Counters {
-  uint32_t rays, shadow, tex;
+  uint32_t rays, shadow, tex, box, prim, wnodes;
 };
 
 struct Ctx {
@@ -981,7 +1001,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     if (have) { out.in_motion = false; cnt.rays++; }   // cpp:519
 
     HitRec h;
-    bool any = closest_hit(S, P, have, ray, eye, shift, h);
+    bool any = closest_hit(S, P, have, ray, eye, shift, h, cnt);
     any = any && have && h.shape >= 0;
     if (have && is_root && any) out.hit = true;
 
@@ -1138,7 +1158,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           cnt.shadow++;
         }
         bool occl = occluded(S, P, lane, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
-                             t_max, L.shape_index, shift);
+                             t_max, L.shape_index, shift, cnt);
         if (lane && !occl) {
           const DMat& M = *Mp;
           GP g = cas(S.geom) + hd.off;
@@ -1287,7 +1307,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   c.rng.k1 = (uint32_t)P.frame;
   unsigned long long sky_px = 0;
   Counters cnt;
-  cnt.rays = 0; cnt.shadow = 0; cnt.tex = 0;
+  cnt.rays = 0; cnt.shadow = 0; cnt.tex = 0; cnt.box = 0; cnt.prim = 0; cnt.wnodes = 0;
 
   while (true) {
     if (lane == 0) item_s = atomicAdd(S.queue, 1ull);
@@ -1420,7 +1440,11 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   }
   {
     unsigned long long r = wave_sum(cnt.rays), sh = wave_sum(cnt.shadow), tx = wave_sum(cnt.tex);
+    unsigned long long bx = wave_sum(cnt.box), pr = wave_sum(cnt.prim);
     if (lane == 0) {
+      atomicAdd(S.stats + ST_BOX, bx);
+      atomicAdd(S.stats + ST_PRIM, pr);
+      atomicAdd(S.stats + ST_WNODES, (unsigned long long)cnt.wnodes);
       if (sky_px) atomicAdd(S.stats + ST_SKY, sky_px);
       atomicAdd(S.stats + ST_RAYS, r);
       atomicAdd(S.stats + ST_SHADOW, sh);

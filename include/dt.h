@@ -215,6 +215,9 @@ typedef struct dt_stats {
   uint64_t nan_pixels;
   uint64_t tex_fetches;       /* texel reads (algorithmic bytes) */
   uint64_t stack_overflows;   /* DFS entries dropped (device stack limit); 0 when validated */
+  uint64_t box_tests;         /* lane-level BVH slab tests (work counter, DESIGN.md roofline) */
+  uint64_t prim_tests;        /* lane-level primitive intersect/intersectShadow calls */
+  uint64_t wave_node_visits;  /* wave-level BVH node visits (union traversal) */
   double   kernel_ms;         /* device time of the render kernels (hipEvents, same stream) */
   double   trace_kernel_ms;   /* device time of the dominant (trace) kernel alone */
 } dt_stats;

@@ -20,4 +20,8 @@ echo write done
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS --kernel-trace -d "$O/sq" -o sq --output-format csv -- python3 $B > "$O/sq.log" 2>&1
 echo sq done
 timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VMEM SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 GRBM_GUI_ACTIVE --kernel-trace -d "$O/sq2" -o sq2 --output-format csv -- python3 $B > "$O/sq2.log" 2>&1 || echo "sq2 pass failed (counter names?)"
+echo sq2 done
+timeout -k 10 400 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA --kernel-trace -d "$O/sq3" -o sq3 --output-format csv -- python3 $B > "$O/sq3.log" 2>&1 || echo "sq3 pass failed"
+echo sq3 done
+timeout -k 10 400 rocprofv3 --pmc SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_SMEM SQ_INST_CYCLES_SALU SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_INT32 --kernel-trace -d "$O/sq4" -o sq4 --output-format csv -- python3 $B > "$O/sq4.log" 2>&1 || echo "sq4 pass failed"
 echo all done
