@@ -98,7 +98,7 @@ class BVHNode(ctypes.Structure):
 # every symbol include/dt.h declares (checked by tests/test_abi.py)
 EXPORTS = ["dt_abi_version", "dt_last_error", "dt_globals_default", "dt_scene_create", "dt_scene_destroy",
            "dt_scene_bvh", "dt_bvh_build", "dt_slab_floats", "dt_slab_floats_max", "dt_render", "dt_render_async",
-           "dt_collect_stats", "dt_render_sky", "dt_unpack_slabs", "dt_build_scene", "dt_scene_desc_free",
+           "dt_collect_stats", "dt_debug_counters", "dt_render_sky", "dt_unpack_slabs", "dt_build_scene", "dt_scene_desc_free",
            "dt_write_ppm", "dt_mocap_bone_table"]
 
 
@@ -129,6 +129,7 @@ def _load():
         "dt_render_async": (c_int32, [ctypes.c_void_p, P(Globals), c_int32, P(Tiles), ctypes.c_void_p,
                                       ctypes.c_void_p]),
         "dt_collect_stats": (c_int32, [ctypes.c_void_p, ctypes.c_void_p, P(Stats)]),
+        "dt_debug_counters": (c_int32, [ctypes.c_void_p, P(c_uint64), c_int32]),
         "dt_render_sky": (c_int32, [P(Globals), c_float, P(Tiles), ctypes.c_void_p, c_int32, ctypes.c_void_p,
                                     P(Stats)]),
         "dt_unpack_slabs": (c_int32, [P(Globals), P(Tiles), c_int32, ctypes.c_void_p, ctypes.c_void_p, c_int32,

@@ -541,3 +541,12 @@ int dt_write_ppm(const char* filename, int32_t xRes, int32_t yRes, const float* 
 }
 
 }  // extern "C"
+
+extern "C" int dt_debug_counters(const dt_scene* sc, uint64_t* out, int32_t n)
+{
+  if (!sc || !out || n < 0 || n > 16) return fail(DT_E_INVALID, "bad arguments");
+  unsigned long long h[ST_N + 16];
+  HIPCHK(hipMemcpy(h, sc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  for (int i = 0; i < n; ++i) out[i] = h[ST_N + 1 + i];
+  return DT_OK;
+}

@@ -835,6 +835,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   const RayBox rb = make_raybox(sray);
   int resume = active ? 0 : 0x7fffffff;
   bool occl = false;
+#ifdef DT_ABL_NOSHADOW
+  return false;
+#endif
   int i = 0;
   const int n_nodes = P.n_nodes;
   while (i < n_nodes) {
@@ -887,7 +890,17 @@ struct PassOut {
 // across the wave once at kernel exit (same-address atomics per lane serialise at L2)
 struct Counters {
   uint32_t rays, shadow, tex, box, prim, wnodes;
+#ifdef DT_STAMPS
+  unsigned long long ph[10];   // diagnostic build only: cycles per phase (wave-uniform)
+#endif
 };
+#ifdef DT_STAMPS
+#define DT_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define DT_ACC(k, a, b) cnt.ph[k] += (b) - (a)
+#else
+#define DT_T(v)
+#define DT_ACC(k, a, b)
+#endif
 
 struct Ctx {
   const DScene* S;
@@ -980,6 +993,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     stack[sp++] = e;
   }
   while (true) {
+    DT_T(t0);
     // pop FINISH entries (own-light contributions), then the next NODE
     bool have = false;
     Entry e;
@@ -1000,8 +1014,12 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     const bool is_root = have && e._pad == 1;
     if (have) { out.in_motion = false; cnt.rays++; }   // cpp:519
 
+    DT_T(t1);
+    DT_ACC(0, t0, t1);
     HitRec h;
     bool any = closest_hit(S, P, have, ray, eye, shift, h, cnt);
+    DT_T(t2);
+    DT_ACC(1, t1, t2);
     any = any && have && h.shape >= 0;
     if (have && is_root && any) out.hit = true;
 
@@ -1138,6 +1156,8 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       }
     }
 
+    DT_T(t3);
+    DT_ACC(2, t2, t3);
     // ---- direct lighting: uniform loop over lights, packet shadow rays (cpp:800-959) ----
     if (__ballot(shade)) {
       const DMat* Mp = S.mat + sid;
@@ -1157,8 +1177,11 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           sn = normalized(sray);
           cnt.shadow++;
         }
+        DT_T(t4);
         bool occl = occluded(S, P, lane, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
                              t_max, L.shape_index, shift, cnt);
+        DT_T(t5);
+        DT_ACC(3, t4, t5);
         if (lane && !occl) {
           const DMat& M = *Mp;
           GP g = cas(S.geom) + hd.off;
@@ -1239,6 +1262,8 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       }
       if (shade && !aborted && hits > 0) own = divs(tmp_color, hits);
     }
+    DT_T(t6);
+    DT_ACC(4, t3, t6);
     if (fin_slot >= 0) {
       Entry f;
       f.a = own; f.b = v3(0, 0, 0); f.k = 0; f.depth = -1; f.key = 0; f._pad = 0;
@@ -1308,6 +1333,9 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   unsigned long long sky_px = 0;
   Counters cnt;
   cnt.rays = 0; cnt.shadow = 0; cnt.tex = 0; cnt.box = 0; cnt.prim = 0; cnt.wnodes = 0;
+#ifdef DT_STAMPS
+  for (int k = 0; k < 10; ++k) cnt.ph[k] = 0;
+#endif
 
   while (true) {
     if (lane == 0) item_s = atomicAdd(S.queue, 1ull);
@@ -1333,6 +1361,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       c.rng.pixel = (uint32_t)(px_y * P.xRes + px_x);
       c.rng.sample = (uint32_t)sample;
 
+      DT_T(k0);
       // camera ray (cpp:1044-1072)
       V3 eye = v3a(P.eye), X = v3a(P.X), Y = v3a(P.Y), Z = v3a(P.Z);
       V3 eye_sample = eye;
@@ -1387,6 +1416,8 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         }
       }
       if (need_blur) tmp_color = divs(tmp_color, P.blur_samples + 1);
+      DT_T(k1);
+      DT_ACC(5, k0, k1);
       const bool miss = valid && !hit0;
       // sky for missing samples: computed once per pixel by the whole wave
       if (P.perlin_cloud) {
@@ -1412,6 +1443,8 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       } else if (miss) {
         tmp_color = v3a(P.default_col);
       }
+      DT_T(k2);
+      DT_ACC(6, k1, k2);
       // ordered per-pixel sum (cpp:1212: color += tmp_color in sample order)
       red[lane * 3 + 0] = tmp_color.x;
       red[lane * 3 + 1] = tmp_color.y;
@@ -1426,6 +1459,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       }
       __syncthreads();
     }
+    DT_T(k3);
     if (lane < group) {
       int qx, qy;
       int64_t qo;
@@ -1445,6 +1479,9 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       atomicAdd(S.stats + ST_BOX, bx);
       atomicAdd(S.stats + ST_PRIM, pr);
       atomicAdd(S.stats + ST_WNODES, (unsigned long long)cnt.wnodes);
+#ifdef DT_STAMPS
+      for (int k = 0; k < 10; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);
+#endif
       if (sky_px) atomicAdd(S.stats + ST_SKY, sky_px);
       atomicAdd(S.stats + ST_RAYS, r);
       atomicAdd(S.stats + ST_SHADOW, sh);

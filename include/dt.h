@@ -264,6 +264,9 @@ int dt_render_async(const dt_scene* s, const dt_globals* g, int32_t frame, const
                     float* out_device, void* stream);
 int dt_collect_stats(const dt_scene* s, void* stream, dt_stats* stats);
 
+/* diagnostic builds (-DDT_STAMPS): per-phase cycle sums of the last render; zeros otherwise */
+int dt_debug_counters(const dt_scene* s, uint64_t* out, int32_t n);
+
 /* renderImageCloud (render_final_project.cpp:1224-1279). Sets eye/up/lookingAt as the
  * reference does (1227-1229) on a local copy; g is not modified. */
 int dt_render_sky(const dt_globals* g, float frame, const dt_tiles* tiles, float* out,

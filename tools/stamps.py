@@ -1,0 +1,32 @@
+"""Diagnostic: phase breakdown of the trace kernel from a -DDT_STAMPS build (DT_LIB=...)."""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import distraytracer_amd as dt  # noqa: E402
+
+NAMES = ["pop", "closest_hit", "hit+children", "occluded", "light loop rest", "sample (passes)", "sky",
+         "-", "-", "-"]
+
+
+def main():
+    g = dt.globals_default()
+    g.use_model = 0
+    b = dt.build_scene("final", 240, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.brdf_samples = 1920, 1080, 64, 8, 2
+    s = dt.Scene(b, g)
+    out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
+    st = dt.render(s, g, 240, out)
+    arr = (ctypes.c_uint64 * 10)()
+    dt.check(dt.lib.dt_debug_counters(s.handle, arr, 10))
+    tot = arr[5] + arr[6]
+    print("kernel ms %.2f" % st.kernel_ms)
+    for i, n in enumerate(NAMES[:7]):
+        print("%-18s %6.2f%%" % (n, 100.0 * arr[i] / max(tot, 1)))
+
+
+if __name__ == "__main__":
+    main()
