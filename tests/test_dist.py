@@ -1,0 +1,70 @@
+"""Multi-rank frame split on CPU (gloo): every rank renders its interleaved 32x32 tiles into a
+packed slab, FrameSplit gathers the slabs to rank 0 and scatters them into the ppmOut image
+(SURVEY §8e). The per-rank renderer here is the oracle (the GPU path is covered by the -m gpu
+tests); what this checks is the N>1 plumbing bench.py runs over RCCL: tile ownership, equal
+slab sizes for a plain gather, the gather itself and the unpack, against the oracle's
+full-frame render. Sample RNG is keyed on the global pixel, so the assembled frame must be
+bit-identical to the single-rank one."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _scene(cfg):
+    import distraytracer_amd as dt
+    g = dt.globals_default()
+    g.use_model = 0
+    if cfg == "final":
+        b = dt.build_scene("final", 240, g)
+        g.xRes, g.yRes, g.antialias_samples, g.max_depth = 72, 40, 4, 3
+    else:
+        b = dt.build_scene("spheres", 0, g)
+        g.xRes, g.yRes, g.antialias_samples, g.max_depth = 70, 45, 1, 1
+    return g, b
+
+
+def _worker(rank, world, port, cfg, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from distraytracer_amd.multigpu import FrameSplit
+        g, b = _scene(cfg)
+        split = FrameSplit(g, world, rank)
+        slab = np.zeros(split.slab_floats, dtype=np.float32)
+        oracle.render(b, g, 240, split.tile, out=slab, nthreads=2)
+        slab_t = torch.from_numpy(slab)
+        gathered = torch.zeros(world * split.slab_floats if rank == 0 else 1, dtype=torch.float32)
+        split.gather(slab_t, gathered if rank == 0 else None)
+        if rank == 0:
+            image = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32)
+            split.assemble(gathered, image)
+            np.save(result_path, image.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cfg", [(2, "final"), (3, "spheres")])
+def test_tile_split_gather_equals_single_rank(tmp_path, world, cfg):
+    import distraytracer_amd as dt
+    import oracle
+    out = str(tmp_path / "img.npy")
+    mp.start_processes(_worker, args=(world, _free_port(), cfg, out), nprocs=world, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    g, b = _scene(cfg)
+    ref, _ = oracle.render(b, g, 240, dt.tiles(), nthreads=4)
+    assert np.array_equal(got, ref)   # bit-identical for any world size
