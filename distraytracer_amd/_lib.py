@@ -106,7 +106,20 @@ class DTError(RuntimeError):
     pass
 
 
+def _share_torch_hip_runtime():
+    """PyTorch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7, but its libraries
+    NEED it as "libamdhip64.so"). If libdt.so is loaded first it binds /opt/rocm's runtime and
+    a later `import torch` loads a second HIP runtime into the process, after which one of the
+    two sees no device. Importing torch first makes libdt's libamdhip64.so.7 dependency
+    resolve to the runtime torch already loaded: one HIP runtime, shared streams/pointers."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def _load():
+    _share_torch_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise DTError("libdt.so not built (%s): run __graft_entry__.build() / make -C "
                       "distraytracer_amd/csrc" % LIB_PATH)

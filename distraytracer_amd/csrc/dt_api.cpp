@@ -182,7 +182,23 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
   const FlatScene& f = s->flat;
   std::vector<int32_t> leaf = f.bvh.leaf_idx;
   if (leaf.empty()) leaf.push_back(0);
-  if ((rc = upload(f.bvh.nodes, &s->d_nodes)) || (rc = upload(leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
+  std::vector<dtd::DNodeDev> dnodes(f.bvh.nodes.size());
+  for (size_t i = 0; i < dnodes.size(); ++i) {
+    const dtd::DNode& n = f.bvh.nodes[i];
+    dtd::DNodeDev& o = dnodes[i];
+    for (int a = 0; a < 3; ++a) { o.lb[a] = n.lb[a]; o.ub[a] = n.ub[a]; }
+    o.skip = n.skip;
+    o.meta = n.leaf ? dtd::DN_LEAF : 0u;
+    o.first = n.first;
+    o.aux = n.count;
+    if (n.leaf && n.count == 1) {
+      const dtd::DShapeHdr& h = f.hdr[f.bvh.leaf_idx[n.first]];
+      o.meta |= dtd::DN_SINGLE | ((uint32_t)h.type << 4) | ((h.flags & 0xffu) << 8);
+      o.first = f.bvh.leaf_idx[n.first];
+      o.aux = h.off;
+    }
+  }
+  if ((rc = upload(dnodes, &s->d_nodes)) || (rc = upload(leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
       (rc = upload(f.geom, &s->d_geom)) || (rc = upload(f.mat, &s->d_mat)) || (rc = upload(f.lights, &s->d_lights)) ||
       (rc = upload(f.tex, &s->d_tex))) {
     dt_scene_destroy(s);

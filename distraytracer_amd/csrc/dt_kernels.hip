@@ -62,7 +62,7 @@ __device__ __forceinline__ const DT_CAS T* cas(const T* p)
 typedef const DT_CAS double* GP;
 
 struct DScene {
-  const DNode* nodes;
+  const DNodeDev* nodes;
   const int32_t* leaf_idx;
   const DShapeHdr* hdr;
   const double* geom;
@@ -73,6 +73,40 @@ struct DScene {
   unsigned long long* stats;
   unsigned long long* queue;
 };
+
+// pow(x, n) for the integer exponents the reference writes as pow(x, 2.0) etc. pow(x, 1) is x
+// and pow(x, 2) is the correctly rounded x*x (glibc's pow is correctly rounded for these,
+// OCML's pow_f64 is not, and its inlined body was the largest source of register spills);
+// higher powers by repeated multiplication (<= 8 roundings, ~1e-14 relative, far inside the
+// 1e-4 parity bound).
+__device__ __forceinline__ double pw1(double x) { return x; }
+__device__ __forceinline__ double pw2(double x) { return x * x; }
+__device__ __forceinline__ double pw3(double x) { return (x * x) * x; }
+__device__ __forceinline__ double pw4(double x) { double x2 = x * x; return x2 * x2; }
+__device__ __forceinline__ double pw5(double x) { double x2 = x * x; return (x2 * x2) * x; }
+__device__ __forceinline__ double pw8(double x) { double x2 = x * x, x4 = x2 * x2; return x4 * x4; }
+__device__ __forceinline__ double pw256(double x)
+{
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x = x * x;
+  return x;
+}
+// pow(x, y) for a runtime exponent (the Phong exponent): small non-negative integers by
+// binary powering, anything else through pow.
+__device__ __forceinline__ double pw_rt(double x, double y)
+{
+  if (y >= 0 && y <= 64 && y == (double)(int)y) {
+    int n = (int)y;
+    double r = 1.0, b = x;
+    while (n) {
+      if (n & 1) r = r * b;
+      n >>= 1;
+      if (n) b = b * b;
+    }
+    return r;
+  }
+  return pow(x, y);
+}
 
 // =====================================================================================
 // value noise (noise.h:25-136) and sky (render_final_project.cpp:146-192)
@@ -148,11 +182,11 @@ __device__ V3 sky_color(const DParams& P, V3 ray)
   V3 sun = v3a(P.sun);
   float sundot = clampf01((float)dot(rnorm, sun));
   double sd = sundot;
-  double p1 = pow(sd, 1.0), p2 = pow(sd, 2.0), p256 = pow(sd, 256.0);
+  double p1 = pw1(sd), p2 = pw2(sd), p256 = pw256(sd);
   V3 term = add(add(mul(p1, mul(0.05, v3a(P.sun_outer))), mul(p2, mul(0.1, v3a(P.sun_inner)))),
                 mul(p256, mul(0.9, v3a(P.sun_core))));
   color = add(color, term);
-  double p8 = pow(sd, 8.0);
+  double p8 = pw8(sd);
   V3 sky = add(mul(1 - 1.5 * p8, v3a(P.bluesky)), mul(p8, mul(1.5, v3a(P.redsky))));
   color = add(color, mul(1.0 - 0.8 * rnorm.y, sky));
   return color;
@@ -178,8 +212,8 @@ __device__ __forceinline__ double cloud_apply(double c, double skyrev, float den
 __device__ V3 cloud_finish(const DParams& P, V3 color)
 {
   color = v3(clampf01((float)color.x), clampf01((float)color.y), clampf01((float)color.z));
-  color = sub(mul(3, v3(pow(color.x, 2.0), pow(color.y, 2.0), pow(color.z, 2.0))),
-              mul(2, v3(pow(color.x, 3.0), pow(color.y, 3.0), pow(color.z, 3.0))));
+  color = sub(mul(3, v3(pw2(color.x), pw2(color.y), pw2(color.z))),
+              mul(2, v3(pw3(color.x), pw3(color.y), pw3(color.z))));
   double s = (color.x + color.y) + color.z;
   V3 grey = v3(0.33 * s, 0.33 * s, 0.33 * s);
   return sub(mul(1 + P.saturation, color), mul(P.saturation, grey));
@@ -263,7 +297,11 @@ struct Rng {
   __device__ void draw(uint32_t node, uint32_t purpose, uint32_t sub, double& u0, double& u1) const
   {
     uint32_t o[4];
-    philox(pixel, sample, node, (purpose << 24) | sub, k0, k1, o);
+    // opaque key: the 10-round key schedule is recomputed per draw (20 SALU adds) instead of
+    // being hoisted into 20 SGPRs that stay live across the whole kernel and spill
+    uint32_t a = k0, b = k1;
+    asm volatile("" : "+s"(a), "+s"(b));
+    philox(pixel, sample, node, (purpose << 24) | sub, a, b, o);
     u0 = u01(o[0], o[1]);
     u1 = u01(o[2], o[3]);
   }
@@ -272,6 +310,7 @@ struct Rng {
 // =====================================================================================
 // primitives (geometry.cpp), geometry from the precomputed pool
 // =====================================================================================
+__device__ __forceinline__ V3 v3a(GP a) { return v3(a[0], a[1], a[2]); }
 __device__ __forceinline__ V3 G3(GP g, int o) { return v3(g[o], g[o + 1], g[o + 2]); }
 
 // Rectangle plane + quad bounds test (geometry.cpp:640-741 / 2292-2312): R record
@@ -326,7 +365,7 @@ __device__ __forceinline__ void shifted_rect(GP g, float shift, V3& A, V3& B,
 // quadratic of Sphere/Cylinder (geometry.cpp:108-124 / 246-256)
 __device__ __forceinline__ bool quad_roots(float A, float B, float C, float& t0, float& t1)
 {
-  float disc = (float)(pow((double)B, 2.0) - (double)(4 * A * C));
+  float disc = (float)(pw2((double)B) - (double)(4 * A * C));
   if (disc < 0) return false;
   float sq = sqrtf(disc);
   t0 = (-B + sq) / (2 * A);
@@ -430,8 +469,8 @@ __device__ bool segment_hit(V3 A, V3 B, V3 ray, V3 origin)
   V3 P3 = add(ray, origin), P4 = origin;
   V3 d13 = sub(A, P3), d43 = sub(P4, P3), d21 = sub(B, A);
   float u1 = (float)((dot(d13, d43) * dot(d43, d21) - dot(d13, d21) * dot(d43, d43)) /
-                     (pow(norm(d21), 2.0) * pow(norm(d43), 2.0) - pow(dot(d43, d21), 2.0)));
-  float u2 = (float)((dot(d13, d43) + u1 * dot(d43, d21)) / pow(norm(d43), 2.0));
+                     (pw2(norm(d21)) * pw2(norm(d43)) - pw2(dot(d43, d21))));
+  float u2 = (float)((dot(d13, d43) + u1 * dot(d43, d21)) / pw2(norm(d43)));
   if (u1 < 0 || u1 > 1) return false;
   if (u2 < 0) return false;
   V3 p1 = add(A, mul(u1, sub(B, A)));
@@ -723,11 +762,10 @@ __device__ __forceinline__ RayBox make_raybox(V3 ray)
 
 // BoundingVolume::intersect (geometry.cpp:2657-2740), branch-free: every early `return false`
 // of the reference becomes a cleared `ok`, every conditional assignment a select, so a wave
-// evaluates one straight-line sequence per node with no exec-mask traffic.
-__device__ __forceinline__ bool box_hit(const DNode& b, float bump, const RayBox& r, V3 st)
+// evaluates one straight-line sequence per node with no exec-mask traffic. lb1/ub1: the
+// y-bounds after the motion-blur leaf bump (helpers.h:530-552).
+__device__ __forceinline__ bool box_hit(const DNodeDev& b, double lb1, double ub1, const RayBox& r, V3 st)
 {
-  double lb1 = b.lb[1], ub1 = b.ub[1];
-  if (b.leaf && bump != 0.0f) { lb1 = lb1 - bump; ub1 = ub1 + bump; }   // bumpBVH (helpers.h:530)
   bool ok;
   float tmin, tmax, tymin, tymax, tzmin, tzmax;
   {
@@ -762,7 +800,69 @@ __device__ __forceinline__ bool box_hit(const DNode& b, float bump, const RayBox
   return ok & (tmax > 0);
 }
 
+// The same test for waves where no lane's ray has a zero component (no isinf(inv) axis, the
+// common case): both slab ends are computed from the unswapped bounds and selected in f32,
+// which yields the identical floats ((lo - st) * inv is evaluated for the same lo either way).
+__device__ __forceinline__ bool box_hit_finite(const DNodeDev& b, double lb1, double ub1, const RayBox& r, V3 st)
+{
+  const float ax = (float)((b.lb[0] - st.x) * r.inv.x), cx = (float)((b.ub[0] - st.x) * r.inv.x);
+  const float ay = (float)((lb1 - st.y) * r.inv.y), cy = (float)((ub1 - st.y) * r.inv.y);
+  const float az = (float)((b.lb[2] - st.z) * r.inv.z), cz = (float)((b.ub[2] - st.z) * r.inv.z);
+  float tmin = r.nx ? cx : ax, tmax = r.nx ? ax : cx;
+  const float tymin = r.ny ? cy : ay, tymax = r.ny ? ay : cy;
+  const float tzmin = r.nz ? cz : az, tzmax = r.nz ? az : cz;
+  bool ok = !((tmin > tymax) | (tymin > tmax));
+  tmin = (tymin > tmin) ? tymin : tmin;
+  tmax = (tymax < tmax) ? tymax : tmax;
+  ok = ok & !((tmin > tzmax) | (tzmin > tmax));
+  tmax = (tzmax < tmax) ? tzmax : tmax;
+  return ok & (tmax > 0);
+}
+
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// wave-uniform traversal state shared by closest_hit / occluded
+struct Walk {
+  RayBox rb;
+  bool inf_wave;   // some lane has an axis-parallel ray: exact isinf path
+  bool bump_wave;  // some lane shifts leaves (motion-blur pass)
+};
+
+__device__ __forceinline__ Walk make_walk(bool active, V3 ray, float shift)
+{
+  Walk w;
+  w.rb = make_raybox(ray);
+  w.inf_wave = __ballot(active && (w.rb.ix | w.rb.iy | w.rb.iz)) != 0;
+  w.bump_wave = __ballot(active && shift != 0.0f) != 0;
+  return w;
+}
+
+__device__ __forceinline__ bool node_hit(const Walk& w, const DNodeDev& nd, float shift, V3 st)
+{
+  double lb1 = nd.lb[1], ub1 = nd.ub[1];
+  if ((nd.meta & DN_LEAF) && w.bump_wave) {   // bumpBVH (helpers.h:530-552): leaves only
+    if (shift != 0.0f) { lb1 = lb1 - shift; ub1 = ub1 + shift; }
+  }
+  return w.inf_wave ? box_hit(nd, lb1, ub1, w.rb, st) : box_hit_finite(nd, lb1, ub1, w.rb, st);
+}
+
+// q-th shape of a leaf: (id, type, flags, geom offset), all wave-uniform
+__device__ __forceinline__ void leaf_shape(const DScene& S, const DNodeDev& nd, int q, int& sid, int& type,
+                                           uint32_t& flags, int& off)
+{
+  if (nd.meta & DN_SINGLE) {
+    sid = nd.first;
+    type = (int)((nd.meta >> 4) & 15u);
+    flags = (nd.meta >> 8) & 0xffu;
+    off = nd.aux;
+  } else {
+    sid = uni(cas(S.leaf_idx)[nd.first + q]);
+    const DShapeHdr hd = cas(S.hdr)[sid];
+    type = hd.type;
+    flags = hd.flags;
+    off = hd.off;
+  }
+}
 
 struct Counters;
 struct HitRec {
@@ -778,7 +878,7 @@ template <class CNT>
 __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 ray, V3 org, float shift,
                                             HitRec& h, CNT& cnt)
 {
-  const RayBox rb = make_raybox(ray);
+  const Walk w = make_walk(active, ray, shift);
   int resume = active ? 0 : 0x7fffffff;
   float t_dist = FLT_MAX;
   bool any = false;
@@ -789,21 +889,23 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
   int i = 0;
   const int n_nodes = P.n_nodes;
   while (i < n_nodes) {
-    const DNode nd = cas(S.nodes)[i];
-    bool act = resume <= i;
-    bool hb = act && box_hit(nd, shift, rb, org);
+    const DNodeDev nd = cas(S.nodes)[i];
+    const bool act = resume <= i;
+    const bool hb = act & node_hit(w, nd, shift, org);
     cnt.wnodes++;
     cnt.box += act;
-    if (nd.leaf) {
+    if (nd.meta & DN_LEAF) {
       if (__ballot(hb)) {
-        for (int q = 0; q < nd.count; ++q) {
-          int sid = uni(cas(S.leaf_idx)[nd.first + q]);
-          DShapeHdr hd = cas(S.hdr)[sid];
+        const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
+        for (int q = 0; q < nq; ++q) {
+          int sid, type, off;
+          uint32_t flags;
+          leaf_shape(S, nd, q, sid, type, flags, off);
           if (hb) {
             cnt.prim++;
             int ins = 0, hc = 0;
             V3 cc;
-            if (shape_hit(S, sid, hd.type, hd.flags, cas(S.geom) + hd.off, ray, org, shift, t_dist, ins, cc, hc)) {
+            if (shape_hit(S, sid, type, flags, cas(S.geom) + off, ray, org, shift, t_dist, ins, cc, hc)) {
               any = true;
               if (t_dist < h.t_min) {
                 h.shape = sid;
@@ -832,7 +934,7 @@ template <class CNT>
 __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
                                          V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
 {
-  const RayBox rb = make_raybox(sray);
+  const Walk w = make_walk(active, sray, shift);
   int resume = active ? 0 : 0x7fffffff;
   bool occl = false;
 #ifdef DT_ABL_NOSHADOW
@@ -841,19 +943,21 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   int i = 0;
   const int n_nodes = P.n_nodes;
   while (i < n_nodes) {
-    const DNode nd = cas(S.nodes)[i];
-    bool act = resume <= i;
-    bool hb = act && box_hit(nd, shift, rb, bstart);
+    const DNodeDev nd = cas(S.nodes)[i];
+    const bool act = resume <= i;
+    const bool hb = act & node_hit(w, nd, shift, bstart);
     cnt.wnodes++;
     cnt.box += act;
-    if (nd.leaf) {
+    if (nd.meta & DN_LEAF) {
       if (__ballot(hb)) {
-        for (int q = 0; q < nd.count; ++q) {
-          int sid = uni(cas(S.leaf_idx)[nd.first + q]);
-          DShapeHdr hd = cas(S.hdr)[sid];
+        const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
+        for (int q = 0; q < nq; ++q) {
+          int sid, type, off;
+          uint32_t flags;
+          leaf_shape(S, nd, q, sid, type, flags, off);
           if (hb && !occl && sid != skip_shape) {
             cnt.prim++;
-            if (shape_shadow(hd.type, hd.flags, cas(S.geom) + hd.off, sn, sstart, t_max, shift)) occl = true;
+            if (shape_shadow(type, flags, cas(S.geom) + off, sn, sstart, t_max, shift)) occl = true;
           }
         }
       }
@@ -937,7 +1041,7 @@ __device__ __forceinline__ V3 rect_sample(V3 A, V3 B, V3 D, double u0, double u1
 }
 
 // light sampleRay (geometry.cpp:2751-2849)
-__device__ V3 light_sample(const Ctx& c, const DLight& L, int li, V3 point, uint32_t node,
+__device__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L, int li, V3 point, uint32_t node,
                            unsigned long long* st_sphl)
 {
   if (L.type == DT_LIGHT_POINT) return sub(v3a(L.center), point);
@@ -975,8 +1079,8 @@ __device__ V3 light_sample(const Ctx& c, const DLight& L, int li, V3 point, uint
 // helpers.h:313-317 (Q10)
 __device__ __forceinline__ float schlick_complex(float cos_theta, double r0, double r1)
 {
-  float R0 = (float)((pow(r0 - 1, 2.0) + pow(r1, 2.0)) / (pow(r0 + 1, 2.0) + pow(r1, 2.0)));
-  return (float)((R0 + (1 - R0)) + pow((double)(1 - cos_theta), 5.0));
+  float R0 = (float)((pw2(r0 - 1) + pw2(r1)) / (pw2(r0 + 1) + pw2(r1)));
+  return (float)((R0 + (1 - R0)) + pw5((double)(1 - cos_theta)));
 }
 
 // One full rayColor tree for the lanes with `active`. Appends to out.color in the
@@ -1071,22 +1175,22 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
             sp = base + nref;
             if (glass) {
               float cos_theta = (float)dot(normal, neg(in));
-              float sin_theta = (float)sqrt(1 - pow((double)cos_theta, 2.0));
+              float sin_theta = (float)sqrt(1 - pw2((double)cos_theta));
               float r1 = h.inside ? P.refr_glass : P.refr_air, r2 = h.inside ? P.refr_air : P.refr_glass;
-              float chk = (float)(1 - pow((double)(r1 / r2), 2.0) * (1 - pow(dot(in, normal), 2.0)));
+              float chk = (float)(1 - pw2((double)(r1 / r2)) * (1 - pw2(dot(in, normal))));
               if (chk >= 0) {
                 float a = r1 / r2 * sin_theta;
                 float b = 1 / sin_theta;
                 float sq = sqrtf(chk);
                 V3 outr = sub(mul(a, mul(b, add(in, mul(cos_theta, normal)))), mul(sq, normal));
                 V3 adj_org = add(isectP, mul(eps, in));
-                float cos_phi = (float)sqrt(1 - pow((double)(P.refr_glass / P.refr_air), 2.0) *
-                                                    (1 - pow(dot(in, normal), 2.0)));
+                float cos_phi = (float)sqrt(1 - pw2((double)(P.refr_glass / P.refr_air)) *
+                                                    (1 - pw2(dot(in, normal))));
                 float rp = (P.refr_glass * cos_theta - P.refr_air * cos_phi) /
                            (P.refr_glass * cos_theta + P.refr_air * cos_phi);
                 float rs = (P.refr_air * cos_theta - P.refr_glass * cos_phi) /
                            (P.refr_air * cos_theta + P.refr_glass * cos_phi);
-                k_refl = (float)(0.5 * (pow((double)rp, 2.0) + pow((double)rs, 2.0)));
+                k_refl = (float)(0.5 * (pw2((double)rp) + pw2((double)rs)));
                 k_refr = 1 - k_refl;
                 Entry ch; ch.a = outr; ch.b = adj_org; ch.k = k_refr * k; ch.depth = depth - 1;
                 ch.key = child_key(node, 0); ch._pad = 0;
@@ -1114,7 +1218,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
                 bool exhausted = false;
                 while (dot(sample_refl, normal) <= 0) {
                   if (sample_limit < 0) { exhausted = true; break; }
-                  float multiplier = (float)pow(2.0, (double)(11 - sample_limit));
+                  float multiplier = (float)ldexp(1.0, 11 - sample_limit);   // pow(2, 11 - limit), exact
                   glossy_rect(refl_ray, isectP, multiplier, A, B, C, D, wv, lv);
                   attempt++;
                   c.rng.draw(node, P_GLOSSY, ((uint32_t)i << 8) | (uint32_t)attempt, u0, u1);
@@ -1140,7 +1244,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       if (M.flags & DT_F_LIGHT) {
         if (M.emit == DT_EMIT_SPHERE) {
           float hitdot = (float)dot(in, normalized(sub(v3a(M.center), isectP)));
-          double f = (0.1 * pow((double)hitdot, 1.0) + 0.05 * pow((double)hitdot, 5.0)) + 0.9;
+          double f = (0.1 * pw1((double)hitdot) + 0.05 * pw5((double)hitdot)) + 0.9;
           own = mul(f, mul(k, shape_color));
         }
         if (M.emit == DT_EMIT_RECT) {
@@ -1148,7 +1252,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           float dist = (float)((((norm(sub(isectP, A)) + norm(sub(isectP, B))) + norm(sub(isectP, C))) +
                                 norm(sub(isectP, D))) /
                                (8 * norm(sub(v3a(M.center), A))));
-          double f = (0.1 * pow((double)dist, 1.0) + 0.05 * pow((double)dist, 5.0)) + 0.9;
+          double f = (0.1 * pw1((double)dist) + 0.05 * pw5((double)dist)) + 0.9;
           own = mul(f, mul(k, shape_color));
         }
       } else {
@@ -1166,7 +1270,8 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       bool aborted = false;
       V3 tmp_color = v3(0, 0, 0);
       for (int li = 0; li < P.n_lights; ++li) {
-        const DLight L = cas(S.lights)[li];
+        // fields are read where used (scalar loads), not held across the shadow walk
+        const DT_CAS DLight& L = cas(S.lights)[li];
         bool lane = shade && !aborted;
         V3 sray = v3(1, 0, 0);
         float t_max = 0;
@@ -1215,8 +1320,8 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
             V3 ray_col;
             const float roughness = M.roughness;
             if (M.model == DT_MODEL_OREN_NAYAR) {
-              float A = (float)(1.0 - (0.5 * pow((double)roughness, 2.0)) / (pow((double)roughness, 2.0) + 0.33));
-              float B = (float)((0.45 * pow((double)roughness, 2.0)) / (pow((double)roughness, 2.0) + 0.09));
+              float A = (float)(1.0 - (0.5 * pw2((double)roughness)) / (pw2((double)roughness) + 0.33));
+              float B = (float)((0.45 * pw2((double)roughness)) / (pw2((double)roughness) + 0.09));
               float vn = (float)dot(e_dir, normal);
               float ln = (float)dot(sn, normal);
               float irradiance = fmaxr(0.0f, ln);
@@ -1233,8 +1338,8 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
               float vn = (float)dot(e_dir, normal);
               float ln = (float)dot(sn, normal);
               float alpha = acosf(hn);
-              float D = (float)(1 / (pow((double)roughness, 2.0) * pow((double)cosf(alpha), 4.0)) *
-                                exp(-pow((double)(tanf(alpha) / roughness), 2.0)));
+              float D = (float)(1 / (pw2((double)roughness) * pw4((double)cosf(alpha))) *
+                                exp(-pw2((double)(tanf(alpha) / roughness))));
               float G1 = (float)(2.0 * hn * vn / vh);
               float G2 = (float)(2.0 * hn * ln / vh);
               float G = 1.0f;
@@ -1249,7 +1354,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
               ray_col = shape_color;
             } else {
               double m1 = dmax(0.0, dot(normal, sn));
-              double pp = pow(dmax(0.0, dot(r, e_dir)), (double)P.phong);
+              double pp = pw_rt(dmax(0.0, dot(r, e_dir)), (double)P.phong);
               V3 shader_rgb = add(mul(m1, lc), mul(pp, lc));
               ray_col = cwise(shape_color, shader_rgb);
             }
@@ -1396,7 +1501,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
             if (P.frame >= P.frame_prism) {   // below frame_prism the reference's val is unset (Q19): 0
               if (P.frame >= P.frame_blur)
                 val = (float)(P.move_per_frame * (frame_sample - P.frame) +
-                              P.accel_t * pow((double)(frame_sample - P.frame), 3.0));
+                              P.accel_t * pw3((double)(frame_sample - P.frame)));
               else
                 val = P.move_per_frame * (frame_sample - P.frame);
             }

@@ -28,6 +28,18 @@ struct alignas(16) DNode {
   int32_t count;  // leaf: number of shapes
 };
 
+// The node as the kernels read it (one 64 B scalar load per visit): the shape header of a
+// single-shape leaf is folded in, so the common leaf costs no dependent leaf_idx -> hdr loads.
+enum { DN_LEAF = 1u, DN_SINGLE = 2u };
+struct alignas(16) DNodeDev {
+  double lb[3];
+  double ub[3];
+  int32_t skip;
+  uint32_t meta;   // bit0 leaf, bit1 single shape, bits 4-7 shape type, bits 8-15 shape flags
+  int32_t first;   // single: shape id ; multi: first entry in leaf_idx
+  int32_t aux;     // single: geom offset ; multi: shape count
+};
+
 struct alignas(16) DShapeHdr {
   int32_t type;
   int32_t off;     // offset into geom[] (doubles)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# build_variant.sh NAME KERNEL.hip [extra hipcc flags...] -> distraytracer_amd/variants/libdt_NAME.so
+# (A/B experiments: same host objects, a different kernel source or flags; see ab_variants.sh)
+set -euo pipefail
+R=$(cd "$(dirname "$0")/.." && pwd)
+C=$R/distraytracer_amd/csrc
+name=$1; src=$2; shift 2
+make -s -C "$C" >/dev/null
+mkdir -p "$R/distraytracer_amd/variants" "$C/build/var"
+/opt/rocm/bin/hipcc -I"$C" -DDT_TRACE_MIN_WAVES=${W:-4} "$@" --offload-arch=gfx950 -O3 -std=c++17 -fPIC \
+  -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -c "$src" -o "$C/build/var/k_$name.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/distraytracer_amd/variants/libdt_$name.so" \
+  "$C/build/var/k_$name.o" "$C"/build/dt_api.o "$C"/build/host_*.o
+echo "built variants/libdt_$name.so"
