@@ -74,7 +74,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frac", type=int, default=16, help="CPU baseline renders 1/N of the tiles")
+    ap.add_argument("--cpu-frac", type=int, default=8, help="CPU baseline renders 1/N of the tiles")
     args = ap.parse_args()
 
     import torch

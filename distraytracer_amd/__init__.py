@@ -44,7 +44,7 @@ class BuiltScene:
         return self._ptr.contents
 
     def __del__(self):
-        if getattr(self, "_ptr", None):
+        if getattr(self, "_ptr", None) and lib is not None:   # lib is None at interpreter exit
             lib.dt_scene_desc_free(self._ptr)
             self._ptr = None
 

@@ -803,10 +803,15 @@ __device__ __forceinline__ bool box_hit(const DNodeDev& b, double lb1, double ub
 // The same test for waves where no lane's ray has a zero component (no isinf(inv) axis, the
 // common case): both slab ends are computed from the unswapped bounds and selected in f32,
 // which yields the identical floats ((lo - st) * inv is evaluated for the same lo either way).
-__device__ __forceinline__ bool box_hit_finite(const DNodeDev& b, double lb1, double ub1, const RayBox& r, V3 st)
+// `tcull` additionally rejects boxes whose entry parameter lies beyond any hit that could
+// still change the result (closest hit: past the best t; shadow: past the light). A shape lies
+// inside its leaf box (bounds of its own vertices/extent, +-1e-2 leaf padding), so a culled box
+// holds no hit the reference would have used: the result is unchanged, only the gather is
+// smaller. Callers pass FLT_MAX to disable it.
+__device__ __forceinline__ bool box_hit_finite(const DNodeDev& b, const RayBox& r, V3 st, float tcull)
 {
   const float ax = (float)((b.lb[0] - st.x) * r.inv.x), cx = (float)((b.ub[0] - st.x) * r.inv.x);
-  const float ay = (float)((lb1 - st.y) * r.inv.y), cy = (float)((ub1 - st.y) * r.inv.y);
+  const float ay = (float)((b.lb[1] - st.y) * r.inv.y), cy = (float)((b.ub[1] - st.y) * r.inv.y);
   const float az = (float)((b.lb[2] - st.z) * r.inv.z), cz = (float)((b.ub[2] - st.z) * r.inv.z);
   float tmin = r.nx ? cx : ax, tmax = r.nx ? ax : cx;
   const float tymin = r.ny ? cy : ay, tymax = r.ny ? ay : cy;
@@ -816,7 +821,8 @@ __device__ __forceinline__ bool box_hit_finite(const DNodeDev& b, double lb1, do
   tmax = (tymax < tmax) ? tymax : tmax;
   ok = ok & !((tmin > tzmax) | (tzmin > tmax));
   tmax = (tzmax < tmax) ? tzmax : tmax;
-  return ok & (tmax > 0);
+  tmin = (tzmin > tmin) ? tzmin : tmin;
+  return ok & (tmax > 0) & (tmin <= tcull);
 }
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -837,13 +843,18 @@ __device__ __forceinline__ Walk make_walk(bool active, V3 ray, float shift)
   return w;
 }
 
-__device__ __forceinline__ bool node_hit(const Walk& w, const DNodeDev& nd, float shift, V3 st)
+// GENERAL: the exact slab test for any wave (axis-parallel rays, motion-blur leaf bump);
+// otherwise the finite-ray test with no bump code at all (the hot instantiation).
+template <bool GENERAL>
+__device__ __forceinline__ bool node_hit(const Walk& w, const DNodeDev& nd, float shift, V3 st, float tcull)
 {
+  if (!GENERAL) return box_hit_finite(nd, w.rb, st, tcull);
   double lb1 = nd.lb[1], ub1 = nd.ub[1];
-  if ((nd.meta & DN_LEAF) && w.bump_wave) {   // bumpBVH (helpers.h:530-552): leaves only
-    if (shift != 0.0f) { lb1 = lb1 - shift; ub1 = ub1 + shift; }
+  if ((nd.meta & DN_LEAF) && shift != 0.0f) {   // bumpBVH (helpers.h:530-552): leaves only
+    lb1 = lb1 - shift;
+    ub1 = ub1 + shift;
   }
-  return w.inf_wave ? box_hit(nd, lb1, ub1, w.rb, st) : box_hit_finite(nd, lb1, ub1, w.rb, st);
+  return box_hit(nd, lb1, ub1, w.rb, st);
 }
 
 // q-th shape of a leaf: (id, type, flags, geom offset), all wave-uniform
@@ -874,11 +885,10 @@ struct HitRec {
 };
 
 // closest hit over the lanes with `active` (cpp:491-538)
-template <class CNT>
-__device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 ray, V3 org, float shift,
-                                            HitRec& h, CNT& cnt)
+template <bool GENERAL, class CNT>
+__device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams& P, const Walk& w, bool active, V3 ray,
+                                                 V3 org, float shift, HitRec& h, CNT& cnt)
 {
-  const Walk w = make_walk(active, ray, shift);
   int resume = active ? 0 : 0x7fffffff;
   float t_dist = FLT_MAX;
   bool any = false;
@@ -891,7 +901,8 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
   while (i < n_nodes) {
     const DNodeDev nd = cas(S.nodes)[i];
     const bool act = resume <= i;
-    const bool hb = act & node_hit(w, nd, shift, org);
+    const float tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
+    const bool hb = act & node_hit<GENERAL>(w, nd, shift, org, tcull);
     cnt.wnodes++;
     cnt.box += act;
     if (nd.meta & DN_LEAF) {
@@ -928,15 +939,26 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
   return any;
 }
 
+template <class CNT>
+__device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 ray, V3 org, float shift,
+                                            HitRec& h, CNT& cnt)
+{
+  const Walk w = make_walk(active, ray, shift);
+  if (w.inf_wave || w.bump_wave) return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
+  return closest_hit_walk<false>(S, P, w, active, ray, org, shift, h, cnt);
+}
+
 // any-hit shadow test (cpp:806-855): box test with sray from isectP+sray*1e-3, shape test
 // with normalized sray from isectP+sn*1e-3, skipping the light's own shape.
-template <class CNT>
-__device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
-                                         V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
+template <bool GENERAL, class CNT>
+__device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P, const Walk& w, bool active, V3 bstart,
+                                              V3 sn, V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
 {
-  const Walk w = make_walk(active, sray, shift);
   int resume = active ? 0 : 0x7fffffff;
   bool occl = false;
+  // an occluder at distance t' < t_max along sn from sstart sits at sray-parameter
+  // u < 1 + 1e-3/|sray| from bstart; margins cover the f32 rounding
+  const float tcull = t_max > 1e-3f ? (1.0f + 1e-3f / t_max) * 1.0001f + 1e-4f : FLT_MAX;
 #ifdef DT_ABL_NOSHADOW
   return false;
 #endif
@@ -945,7 +967,7 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   while (i < n_nodes) {
     const DNodeDev nd = cas(S.nodes)[i];
     const bool act = resume <= i;
-    const bool hb = act & node_hit(w, nd, shift, bstart);
+    const bool hb = act & node_hit<GENERAL>(w, nd, shift, bstart, tcull);
     cnt.wnodes++;
     cnt.box += act;
     if (nd.meta & DN_LEAF) {
@@ -970,6 +992,16 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
     if (!__ballot(resume != 0x7fffffff)) break;
   }
   return occl;
+}
+
+template <class CNT>
+__device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
+                                         V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
+{
+  const Walk w = make_walk(active, sray, shift);
+  if (w.inf_wave || w.bump_wave)
+    return occluded_walk<true>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+  return occluded_walk<false>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 }
 
 // =====================================================================================

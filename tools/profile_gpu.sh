@@ -24,4 +24,5 @@ echo sq2 done
 timeout -k 10 400 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA --kernel-trace -d "$O/sq3" -o sq3 --output-format csv -- python3 $B > "$O/sq3.log" 2>&1 || echo "sq3 pass failed"
 echo sq3 done
 timeout -k 10 400 rocprofv3 --pmc SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_SMEM SQ_INST_CYCLES_SALU SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_INT32 --kernel-trace -d "$O/sq4" -o sq4 --output-format csv -- python3 $B > "$O/sq4.log" 2>&1 || echo "sq4 pass failed"
+timeout -k 10 400 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCC_HIT_sum TCC_MISS_sum SQC_ICACHE_MISSES SQC_DCACHE_MISSES --kernel-trace -d "$O/l2" -o l2 --output-format csv -- python3 $B > "$O/l2.log" 2>&1 || echo "l2 pass failed"
 echo all done
