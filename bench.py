@@ -62,7 +62,8 @@ def load_pmc_traffic():
         return None
     try:
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            d = json.load(f)
+        return d
     except Exception:
         return None
 
@@ -152,7 +153,8 @@ def main():
         alg_bytes = px * 3 * 4 + lib_stats.tex_fetches * 3 + 70 * 1024
         achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
         peak = 8000.0
-        traffic = load_pmc_traffic()
+        pmc = load_pmc_traffic() or {}
+        traffic = pmc.get("hbm_bytes_per_launch")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(dt, args.config, args.cpu_frac)
@@ -176,6 +178,10 @@ def main():
                        "parallelism": "tile-split x%d + RCCL gather" % world if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 4), "peak": peak, "unit": "GB/s",
                          "frac": achieved / peak, "traffic": traffic,
+                         "traffic_source": ("profiles/%s_summary.json (2*FETCH_SIZE + WRITE_SIZE, fabric requests "
+                                            "incl. Infinity-Cache hits: an upper bound on HBM bytes)" % pmc.get("tag"))
+                         if traffic else None,
+                         "valu_active_per_wave_cycle": pmc.get("valu_active_per_wave_cycle"),
                          "kernel": "dt_trace_kernel", "kernel_ms": round(kernel_ms, 3),
                          "alg_bytes_per_launch": int(alg_bytes),
                          "note": "VALU-bound path (FP64 intersection/shading); HBM fraction reported as "

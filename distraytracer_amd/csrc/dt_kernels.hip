@@ -813,16 +813,13 @@ __device__ __forceinline__ bool box_hit_finite(const DNodeDev& b, const RayBox& 
   const float ax = (float)((b.lb[0] - st.x) * r.inv.x), cx = (float)((b.ub[0] - st.x) * r.inv.x);
   const float ay = (float)((b.lb[1] - st.y) * r.inv.y), cy = (float)((b.ub[1] - st.y) * r.inv.y);
   const float az = (float)((b.lb[2] - st.z) * r.inv.z), cz = (float)((b.ub[2] - st.z) * r.inv.z);
-  float tmin = r.nx ? cx : ax, tmax = r.nx ? ax : cx;
-  const float tymin = r.ny ? cy : ay, tymax = r.ny ? ay : cy;
-  const float tzmin = r.nz ? cz : az, tzmax = r.nz ? az : cz;
-  bool ok = !((tmin > tymax) | (tymin > tmax));
-  tmin = (tymin > tmin) ? tymin : tmin;
-  tmax = (tymax < tmax) ? tymax : tmax;
-  ok = ok & !((tmin > tzmax) | (tzmin > tmax));
-  tmax = (tzmax < tmax) ? tzmax : tmax;
-  tmin = (tzmin > tmin) ? tzmin : tmin;
-  return ok & (tmax > 0) & (tmin <= tcull);
+  // The reference's slab sequence accepts iff every entry value <= every exit value
+  // (tx_min <= ty_max, ty_min <= tx_max, max(..) <= tz_max, tz_min <= min(..)) and the
+  // final exit > 0: i.e. max3(entries) <= min3(exits) && min3(exits) > 0. No NaN can occur
+  // here (finite inverse), and +-0 compare equal, so the min/max form decides identically.
+  const float tmin = fmaxf(fmaxf(r.nx ? cx : ax, r.ny ? cy : ay), r.nz ? cz : az);
+  const float tmax = fminf(fminf(r.nx ? ax : cx, r.ny ? ay : cy), r.nz ? az : cz);
+  return (tmin <= tmax) & (tmax > 0) & (tmin <= tcull);
 }
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -834,11 +831,15 @@ struct Walk {
   bool bump_wave;  // some lane shifts leaves (motion-blur pass)
 };
 
-__device__ __forceinline__ Walk make_walk(bool active, V3 ray, float shift)
+// inf_wave also takes NaN rays/origins: the reference's slab sequence treats a NaN axis
+// asymmetrically (x fails, y/z are skipped), which only the exact general test reproduces.
+__device__ __forceinline__ Walk make_walk(bool active, V3 ray, V3 st, float shift)
 {
   Walk w;
   w.rb = make_raybox(ray);
-  w.inf_wave = __ballot(active && (w.rb.ix | w.rb.iy | w.rb.iz)) != 0;
+  const bool odd = w.rb.ix | w.rb.iy | w.rb.iz | isnan(ray.x) | isnan(ray.y) | isnan(ray.z) | isnan(st.x) |
+                   isnan(st.y) | isnan(st.z);
+  w.inf_wave = __ballot(active && odd) != 0;
   w.bump_wave = __ballot(active && shift != 0.0f) != 0;
   return w;
 }
@@ -943,7 +944,7 @@ template <class CNT>
 __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 ray, V3 org, float shift,
                                             HitRec& h, CNT& cnt)
 {
-  const Walk w = make_walk(active, ray, shift);
+  const Walk w = make_walk(active, ray, org, shift);
   if (w.inf_wave || w.bump_wave) return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
   return closest_hit_walk<false>(S, P, w, active, ray, org, shift, h, cnt);
 }
@@ -977,7 +978,8 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
           int sid, type, off;
           uint32_t flags;
           leaf_shape(S, nd, q, sid, type, flags, off);
-          if (hb && !occl && sid != skip_shape) {
+          const bool test = hb && !occl && sid != skip_shape;
+          if (test) {
             cnt.prim++;
             if (shape_shadow(type, flags, cas(S.geom) + off, sn, sstart, t_max, shift)) occl = true;
           }
@@ -998,7 +1000,7 @@ template <class CNT>
 __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
                                          V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
 {
-  const Walk w = make_walk(active, sray, shift);
+  const Walk w = make_walk(active, sray, bstart, shift);
   if (w.inf_wave || w.bump_wave)
     return occluded_walk<true>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
   return occluded_walk<false>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
@@ -1025,7 +1027,9 @@ struct PassOut {
 // per-lane event counters, kept in registers for the whole persistent loop and reduced
 // across the wave once at kernel exit (same-address atomics per lane serialise at L2)
 struct Counters {
-  uint32_t rays, shadow, tex, box, prim, wnodes;
+  uint32_t rays, shadow, tex;        // per lane, wave-summed at exit
+  uint32_t box, prim;
+  uint32_t wnodes;                   // wave-level
 #ifdef DT_STAMPS
   unsigned long long ph[10];   // diagnostic build only: cycles per phase (wave-uniform)
 #endif

@@ -54,6 +54,11 @@ def main(tag, kernel="dt_trace_kernel"):
         json.dump(out, fh, indent=1, sort_keys=True)
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(ROOT, "profiles", "%s_kernel_stats.csv" % tag))
+    # the profile bench.py's roofline.traffic reads (the latest summarised tag)
+    with open(os.path.join(ROOT, "profiles", "pmc_trace_summary.json"), "w") as fh:
+        json.dump({k: out.get(k) for k in ("tag", "kernel", "avg_duration_ns", "hbm_bytes_per_launch",
+                                            "valu_active_per_wave_cycle", "valu_lane_utilisation")},
+                  fh, indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
     return out
 
