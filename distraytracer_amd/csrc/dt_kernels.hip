@@ -1305,10 +1305,36 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       int hits = 0;
       bool aborted = false;
       V3 tmp_color = v3(0, 0, 0);
+      // Textured hits: getUV and the texel depend only on the hit point, so they are evaluated
+      // once per node; the reference repeats them for every unoccluded light (cpp:859-893) with
+      // the same result. A UV type 0 makes the node's own light 0 whichever lights are
+      // unoccluded (Q8 abort, or no hits at all), so such lanes trace no shadow rays.
+      int uvt = 1;
+      double tu = 0, tv = 0;
+      V3 tex_color = shape_color;
+      const bool textured = shade && (Mp->flags & DT_F_TEXTURE);
+      if (textured) {
+        const DMat& M = *Mp;
+        uvt = shape_uv(hd.type, hd.flags, cas(S.geom) + hd.off, isectP, shift, tu, tv);
+        if (uvt == 2) {
+          tex_color = v3a(M.bordercolor);
+        } else if (uvt == 1 && M.tex >= 0) {
+          double dims0 = M.tex_w;
+          int x_tex = (int)((float)(M.tex_w - 1) * (float)tu);
+          int y_tex = (int)((float)(M.tex_h - 1) * (float)tv);
+          int uv_ind = (int)(y_tex * dims0 + x_tex);
+          if (uv_ind < 0) uv_ind = 0;
+          if (uv_ind >= M.tex_w * M.tex_h) uv_ind = M.tex_w * M.tex_h - 1;
+          const uint8_t* px = S.tex + M.tex_off + (int64_t)uv_ind * M.tex_ch;
+          tex_color = v3(px[0] / 255.0, px[1] / 255.0, px[2] / 255.0);
+        }
+      }
+      const bool uv_oob = textured && uvt != 0 && (tu < 0 || tv < 0 || tu > 1 || tv > 1);
+      const bool tex_applies = textured && (uvt == 2 || (uvt == 1 && Mp->tex >= 0));
       for (int li = 0; li < P.n_lights; ++li) {
         // fields are read where used (scalar loads), not held across the shadow walk
         const DT_CAS DLight& L = cas(S.lights)[li];
-        bool lane = shade && !aborted;
+        bool lane = shade && !aborted && uvt != 0;
         V3 sray = v3(1, 0, 0);
         float t_max = 0;
         V3 sn = v3(1, 0, 0);
@@ -1325,34 +1351,15 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
         DT_ACC(3, t4, t5);
         if (lane && !occl) {
           const DMat& M = *Mp;
-          GP g = cas(S.geom) + hd.off;
           V3 lc = v3a(L.color);
-          V3 r = normalized(add(mul(-1, sray), mul(2 * dot(normal, sray), normal)));
-          bool skip_rest = false;
-          if (M.flags & DT_F_TEXTURE) {
-            double u, v;
-            int type = shape_uv(hd.type, hd.flags, g, isectP, shift, u, v);
-            if (type == 0) {
-              aborted = true;   // Q8: `return` discards this node's lighting
-              skip_rest = true;
-            } else {
-              if (u < 0 || v < 0 || u > 1 || v > 1) atomicAdd(S.stats + ST_UV, 1ull);
-              if (type == 2) {
-                shape_color = v3a(M.bordercolor);
-              } else if (type == 1 && M.tex >= 0) {
-                double dims0 = M.tex_w;
-                int x_tex = (int)((float)(M.tex_w - 1) * (float)u);
-                int y_tex = (int)((float)(M.tex_h - 1) * (float)v);
-                int uv_ind = (int)(y_tex * dims0 + x_tex);
-                if (uv_ind < 0) uv_ind = 0;
-                if (uv_ind >= M.tex_w * M.tex_h) uv_ind = M.tex_w * M.tex_h - 1;
-                const uint8_t* px = S.tex + M.tex_off + (int64_t)uv_ind * M.tex_ch;
-                cnt.tex++;
-                shape_color = v3(px[0] / 255.0, px[1] / 255.0, px[2] / 255.0);
-              }
+          if (textured) {
+            if (uv_oob) atomicAdd(S.stats + ST_UV, 1ull);   // the reference terminates here (Q9)
+            if (tex_applies) {
+              shape_color = tex_color;
+              if (uvt == 1) cnt.tex++;
             }
           }
-          if (!skip_rest) {
+          {
             V3 ray_col;
             const float roughness = M.roughness;
             if (M.model == DT_MODEL_OREN_NAYAR) {
@@ -1389,6 +1396,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
             } else if (M.model == DT_MODEL_RAW) {
               ray_col = shape_color;
             } else {
+              V3 r = normalized(add(mul(-1, sray), mul(2 * dot(normal, sray), normal)));
               double m1 = dmax(0.0, dot(normal, sn));
               double pp = pw_rt(dmax(0.0, dot(r, e_dir)), (double)P.phong);
               V3 shader_rgb = add(mul(m1, lc), mul(pp, lc));
