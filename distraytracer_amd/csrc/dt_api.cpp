@@ -298,6 +298,7 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   zs = cloud_z_steps(*g);
   if (g->perlin_cloud && zs.size() > 2048) return fail(DT_E_LIMIT, "clouddist/0.05 exceeds 2048 march steps");
   P.n_nodes = (int32_t)sc->flat.bvh.nodes.size();
+
   P.n_lights = (int32_t)sc->flat.lights.size();
   P.n_shapes = (int32_t)sc->flat.hdr.size();
   return DT_OK;

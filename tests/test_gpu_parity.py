@@ -80,6 +80,21 @@ def test_spheres_c1_dof(cuda):
     _cmp(gpu, ref, 0.0005, "spheres C1 dof")
 
 
+def test_spheres_motion_blur_shift(cuda):
+    """Motion-blur re-traces with a non-zero shift: buildSceneSpheres(0) rendered at frame 1700
+    (>= frame_blur, so val = move_per_frame*dt + accel_t*dt^3, Q19): every leaf box is bumped by
+    +-val in y (bumpBVH, helpers.h:530-552), which runs the device's general traversal path."""
+    g = dt.globals_default()
+    built = dt.build_scene("spheres", 0, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = 128, 128, 4, 2
+    assert g.blur_samples > 0
+    tile = dt.tiles()
+    gpu, st = _render_gpu(built, g, 1700, tile)
+    ref, _ = oracle.render(built, g, 1700, tile)
+    assert st.rays > st.samples   # the re-traces ran
+    _cmp(gpu, ref, 0.001, "spheres motion blur frame 1700")
+
+
 @pytest.mark.parametrize("window", [(380, 250, 420, 280), (100, 400, 140, 430), (700, 100, 740, 130),
                                    (560, 420, 600, 450)])
 def test_final_c2_windows(cuda, window):
