@@ -32,6 +32,17 @@ using namespace dtd;
 #define M_PI 3.14159265358979323846
 #endif
 
+// diagnostic build (-DDT_STAMPS): per-phase cycle sums and wave-level event counts
+#ifdef DT_STAMPS
+#define DT_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define DT_ACC(k, a, b) cnt.ph[k] += (b) - (a)
+#define DT_CNT(k) cnt.ph[k] += 1   // wave-uniform event count (7 DFS steps, 8 prim tests, 9 lights)
+#else
+#define DT_CNT(k)
+#define DT_T(v)
+#define DT_ACC(k, a, b)
+#endif
+
 #define DT_STACK_MAX 48
 #define DT_MAX_CLOUD_STEPS 2048
 #define DT_WAVE 64
@@ -929,6 +940,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
           int sid, type, off;
           uint32_t flags;
           leaf_shape(S, nd, q, sid, type, flags, off);
+          DT_CNT(8);
           if (hb) {
             cnt.prim++;
             int ins = 0, hc = 0;
@@ -994,6 +1006,7 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
           int sid, type, off;
           uint32_t flags;
           leaf_shape(S, nd, q, sid, type, flags, off);
+          DT_CNT(8);
           const bool test = hb && !occl && sid != skip_shape;
           if (test) {
             cnt.prim++;
@@ -1050,13 +1063,6 @@ struct Counters {
   unsigned long long ph[10];   // diagnostic build only: cycles per phase (wave-uniform)
 #endif
 };
-#ifdef DT_STAMPS
-#define DT_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define DT_ACC(k, a, b) cnt.ph[k] += (b) - (a)
-#else
-#define DT_T(v)
-#define DT_ACC(k, a, b)
-#endif
 
 struct Ctx {
   const DScene* S;
@@ -1163,6 +1169,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       }
     }
     if (!__ballot(have)) break;
+    DT_CNT(7);
     const V3 ray = e.a, eye = e.b;
     const int depth = e.depth;
     const float k = e.k;
@@ -1346,26 +1353,39 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
         }
       }
       const bool uv_oob = textured && uvt != 0 && (tu < 0 || tv < 0 || tu > 1 || tv > 1);
+      const int model = shade ? Mp->model : DT_MODEL_RAW;
+      const bool phong_lane = model != DT_MODEL_OREN_NAYAR && model != DT_MODEL_COOK_TORRANCE && model != DT_MODEL_RAW;
       const bool tex_applies = textured && (uvt == 2 || (uvt == 1 && Mp->tex >= 0));
       for (int li = 0; li < P.n_lights; ++li) {
         // fields are read where used (scalar loads), not held across the shadow walk
         const DT_CAS DLight& L = cas(S.lights)[li];
+        DT_CNT(9);
         bool lane = shade && !aborted && uvt != 0;
         V3 sray = v3(1, 0, 0);
         float t_max = 0;
         V3 sn = v3(1, 0, 0);
+        bool dark = false;   // Phong term provably exactly 0: occlusion cannot matter
         if (lane) {
           sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL);
           t_max = (float)norm(sray);
           sn = normalized(sray);
           cnt.shadow++;
+          // Phong (cpp:943-948): m1 = max(0, n.sn) and pp = max(0, r.e)^phong are both 0 when
+          // the light sample is behind the surface and its mirror direction points away from
+          // the eye; then ray_col is exactly 0 and the light is not counted (isApprox(0),
+          // Q7) whether or not it is occluded, so the shadow walk is skipped. NaNs fail the
+          // <= tests and take the normal path.
+          if (phong_lane && dot(normal, sn) <= 0) {
+            V3 r = normalized(add(mul(-1, sray), mul(2 * dot(normal, sray), normal)));
+            dark = dot(r, e_dir) <= 0;
+          }
         }
         DT_T(t4);
-        bool occl = occluded(S, P, lane, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
+        bool occl = occluded(S, P, lane && !dark, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
                              t_max, L.shape_index, shift, cnt);
         DT_T(t5);
         DT_ACC(3, t4, t5);
-        if (lane && !occl) {
+        if (lane && !dark && !occl) {
           const DMat& M = *Mp;
           V3 lc = v3a(L.color);
           if (textured) {

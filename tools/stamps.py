@@ -26,6 +26,9 @@ def main():
     print("kernel ms %.2f" % st.kernel_ms)
     for i, n in enumerate(NAMES[:7]):
         print("%-18s %6.2f%%" % (n, 100.0 * arr[i] / max(tot, 1)))
+    items = g.xRes * g.yRes   # one wave item per pixel at 64 spp
+    print("per wave item: DFS steps %.2f  wave-level prim tests %.2f  light iterations %.2f  node visits %.1f"
+          % (arr[7] / items, arr[8] / items, arr[9] / items, st.wave_node_visits / items))
 
 
 if __name__ == "__main__":
