@@ -45,6 +45,7 @@ using namespace dtd;
 
 #define DT_STACK_MAX 48
 #define DT_MAX_CLOUD_STEPS 2048
+#define DT_CLOUD_CHUNK 256
 #define DT_WAVE 64
 
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
@@ -252,19 +253,25 @@ __device__ V3 cloud_color_lane(const DParams& P, const float* __restrict__ zs, V
 __device__ V3 cloud_color_coop(const DParams& P, const float* __restrict__ zs, V3 ray,
                                float* __restrict__ dens, double* __restrict__ chan)
 {
+  // the march in chunks of DT_CLOUD_CHUNK steps: densities in parallel over the lanes, then
+  // the per-channel recurrence on lanes 0-2 in step order (same arithmetic as one pass)
   const int lane = threadIdx.x & 63;
   V3 sky = sky_color(P, ray);
-  for (int s = lane; s < P.n_cloud_steps; s += DT_WAVE) dens[s] = cloud_step(P, zs[s], ray);
-  __syncthreads();
-  if (lane < 3) {
-    double c = lane == 0 ? sky.x : (lane == 1 ? sky.y : sky.z);
-    double rev = lane == 0 ? sky.z : (lane == 1 ? sky.y : sky.x);
-    for (int s = 0; s < P.n_cloud_steps; ++s) {
-      float d = dens[s];
-      if (d >= 0.0f) c = cloud_apply(c, rev, d);
+  double c = lane == 0 ? sky.x : (lane == 1 ? sky.y : sky.z);
+  const double rev = lane == 0 ? sky.z : (lane == 1 ? sky.y : sky.x);
+  for (int s0 = 0; s0 < P.n_cloud_steps; s0 += DT_CLOUD_CHUNK) {
+    const int n = P.n_cloud_steps - s0 < DT_CLOUD_CHUNK ? P.n_cloud_steps - s0 : DT_CLOUD_CHUNK;
+    for (int s = lane; s < n; s += DT_WAVE) dens[s] = cloud_step(P, zs[s0 + s], ray);
+    __syncthreads();
+    if (lane < 3) {
+      for (int s = 0; s < n; ++s) {
+        float d = dens[s];
+        if (d >= 0.0f) c = cloud_apply(c, rev, d);
+      }
     }
-    chan[lane] = c;
+    __syncthreads();
   }
+  if (lane < 3) chan[lane] = c;
   __syncthreads();
   V3 col = v3(chan[0], chan[1], chan[2]);
   __syncthreads();
@@ -1117,7 +1124,7 @@ __device__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L, int li, V3 poin
   V3 tmp = add(mul(L.radius, dir), C);
   int sample_limit = 20;
   while (dot(sub(tmp, C), sub(point, C)) < 0 || (L.use_baxis && dot(sub(tmp, C), baxis) < 0)) {
-    if (sample_limit < 0) { atomicAdd(st_sphl, 1ull); break; }
+    if (sample_limit < 0) { if (st_sphl) atomicAdd(st_sphl, 1ull); break; }
     V3 rev = add(mul(-L.radius, dir), C);
     if (dot(sub(rev, C), sub(point, C)) >= 0 && (!L.use_baxis || dot(sub(rev, C), baxis) >= 0)) {
       tmp = rev;
@@ -1144,7 +1151,7 @@ __device__ __forceinline__ float schlick_complex(float cos_theta, double r0, dou
 // One full rayColor tree for the lanes with `active`. Appends to out.color in the
 // reference's accumulation order.
 __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t rootkey, float shift,
-                         PassOut& out, Entry* stack, Counters& cnt)
+                         PassOut& out, Entry* stack, Counters& cnt, double (*nrec)[DT_WAVE])
 {
   const DScene& S = *c.S;
   const DParams& P = *c.P;
@@ -1321,131 +1328,137 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
 
     DT_T(t3);
     DT_ACC(2, t2, t3);
-    // ---- direct lighting: uniform loop over lights, packet shadow rays (cpp:800-959) ----
+    // ---- direct lighting (cpp:800-959) ------------------------------------------------
+    // Two passes over the lights. Pass 1 walks one packet shadow ray per light and keeps only
+    // a visibility bit; the shading inputs (normal, eye, colour) are parked in LDS meanwhile,
+    // so the walks run with a small live register set instead of spilling the BRDF state to
+    // scratch around every walk. Pass 2 regenerates each unoccluded light sample (counter RNG:
+    // the same values) and evaluates the BRDFs in light order, as the reference's loop does.
     if (__ballot(shade)) {
-      const DMat* Mp = S.mat + sid;
-      V3 e_dir = normalized(sub(eye, isectP));
-      int hits = 0;
-      bool aborted = false;
-      V3 tmp_color = v3(0, 0, 0);
-      // Textured hits: getUV and the texel depend only on the hit point, so they are evaluated
-      // once per node; the reference repeats them for every unoccluded light (cpp:859-893) with
-      // the same result. A UV type 0 makes the node's own light 0 whichever lights are
-      // unoccluded (Q8 abort, or no hits at all), so such lanes trace no shadow rays.
+      // getUV/texel depend only on the hit point: once per node (the reference repeats them
+      // per unoccluded light with the same result). UV type 0 makes the node's own light 0
+      // whichever lights are visible (Q8 abort, or no hits), so such lanes walk nothing.
       int uvt = 1;
       double tu = 0, tv = 0;
-      V3 tex_color = shape_color;
-      const bool textured = shade && (Mp->flags & DT_F_TEXTURE);
-      if (textured) {
-        const DMat& M = *Mp;
-        uvt = shape_uv(hd.type, hd.flags, cas(S.geom) + hd.off, isectP, shift, tu, tv);
-        if (uvt == 2) {
-          tex_color = v3a(M.bordercolor);
-        } else if (uvt == 1 && M.tex >= 0) {
-          double dims0 = M.tex_w;
-          int x_tex = (int)((float)(M.tex_w - 1) * (float)tu);
-          int y_tex = (int)((float)(M.tex_h - 1) * (float)tv);
-          int uv_ind = (int)(y_tex * dims0 + x_tex);
-          if (uv_ind < 0) uv_ind = 0;
-          if (uv_ind >= M.tex_w * M.tex_h) uv_ind = M.tex_w * M.tex_h - 1;
-          const uint8_t* px = S.tex + M.tex_off + (int64_t)uv_ind * M.tex_ch;
-          tex_color = v3(px[0] / 255.0, px[1] / 255.0, px[2] / 255.0);
-        }
+      const bool textured = shade && (S.mat[sid].flags & DT_F_TEXTURE);
+      if (textured) uvt = shape_uv(hd.type, hd.flags, cas(S.geom) + hd.off, isectP, shift, tu, tv);
+      const bool walk = shade && uvt != 0;
+      const int ln_ = threadIdx.x & (DT_WAVE - 1);
+      if (walk) {
+        nrec[0][ln_] = normal.x; nrec[1][ln_] = normal.y; nrec[2][ln_] = normal.z;
+        nrec[3][ln_] = eye.x; nrec[4][ln_] = eye.y; nrec[5][ln_] = eye.z;
+        nrec[6][ln_] = shape_color.x; nrec[7][ln_] = shape_color.y; nrec[8][ln_] = shape_color.z;
       }
-      const bool uv_oob = textured && uvt != 0 && (tu < 0 || tv < 0 || tu > 1 || tv > 1);
-      const int model = shade ? Mp->model : DT_MODEL_RAW;
-      const bool phong_lane = model != DT_MODEL_OREN_NAYAR && model != DT_MODEL_COOK_TORRANCE && model != DT_MODEL_RAW;
-      const bool tex_applies = textured && (uvt == 2 || (uvt == 1 && Mp->tex >= 0));
+      asm volatile("" ::: "memory");
+      uint32_t vis = 0;
       for (int li = 0; li < P.n_lights; ++li) {
-        // fields are read where used (scalar loads), not held across the shadow walk
         const DT_CAS DLight& L = cas(S.lights)[li];
         DT_CNT(9);
-        bool lane = shade && !aborted && uvt != 0;
         V3 sray = v3(1, 0, 0);
         float t_max = 0;
         V3 sn = v3(1, 0, 0);
-        bool dark = false;   // Phong term provably exactly 0: occlusion cannot matter
-        if (lane) {
+        if (walk) {
           sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL);
           t_max = (float)norm(sray);
           sn = normalized(sray);
           cnt.shadow++;
-          // Phong (cpp:943-948): m1 = max(0, n.sn) and pp = max(0, r.e)^phong are both 0 when
-          // the light sample is behind the surface and its mirror direction points away from
-          // the eye; then ray_col is exactly 0 and the light is not counted (isApprox(0),
-          // Q7) whether or not it is occluded, so the shadow walk is skipped. NaNs fail the
-          // <= tests and take the normal path.
-          if (phong_lane && dot(normal, sn) <= 0) {
-            V3 r = normalized(add(mul(-1, sray), mul(2 * dot(normal, sray), normal)));
-            dark = dot(r, e_dir) <= 0;
-          }
         }
         DT_T(t4);
-        bool occl = occluded(S, P, lane && !dark, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
+        bool occl = occluded(S, P, walk, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
                              t_max, L.shape_index, shift, cnt);
         DT_T(t5);
         DT_ACC(3, t4, t5);
-        if (lane && !dark && !occl) {
+        if (walk && !occl) vis |= 1u << li;
+      }
+      asm volatile("" ::: "memory");
+      if (__ballot(vis != 0)) {
+        V3 nrm = v3(0, 0, 0), eye2 = v3(0, 0, 0);
+        if (vis != 0) {
+          nrm = v3(nrec[0][ln_], nrec[1][ln_], nrec[2][ln_]);
+          eye2 = v3(nrec[3][ln_], nrec[4][ln_], nrec[5][ln_]);
+          shape_color = v3(nrec[6][ln_], nrec[7][ln_], nrec[8][ln_]);
+        }
+        const DMat* Mp = S.mat + sid;
+        const V3 e_dir = normalized(sub(eye2, isectP));
+        const bool uv_oob = textured && (tu < 0 || tv < 0 || tu > 1 || tv > 1);
+        if (vis != 0 && textured) {
           const DMat& M = *Mp;
+          if (uvt == 2) {
+            shape_color = v3a(M.bordercolor);
+          } else if (uvt == 1 && M.tex >= 0) {
+            double dims0 = M.tex_w;
+            int x_tex = (int)((float)(M.tex_w - 1) * (float)tu);
+            int y_tex = (int)((float)(M.tex_h - 1) * (float)tv);
+            int uv_ind = (int)(y_tex * dims0 + x_tex);
+            if (uv_ind < 0) uv_ind = 0;
+            if (uv_ind >= M.tex_w * M.tex_h) uv_ind = M.tex_w * M.tex_h - 1;
+            const uint8_t* px = S.tex + M.tex_off + (int64_t)uv_ind * M.tex_ch;
+            shape_color = v3(px[0] / 255.0, px[1] / 255.0, px[2] / 255.0);
+          }
+        }
+        int hits = 0;
+        V3 tmp_color = v3(0, 0, 0);
+        for (int li = 0; li < P.n_lights; ++li) {
+          if (!(vis & (1u << li))) continue;
+          const DT_CAS DLight& L = cas(S.lights)[li];
+          const DMat& M = *Mp;
+          const V3 sray = light_sample(c, L, li, isectP, node, nullptr);
+          const V3 sn = normalized(sray);
+          const V3 normal = nrm;
           V3 lc = v3a(L.color);
           if (textured) {
             if (uv_oob) atomicAdd(S.stats + ST_UV, 1ull);   // the reference terminates here (Q9)
-            if (tex_applies) {
-              shape_color = tex_color;
-              if (uvt == 1) cnt.tex++;
-            }
+            if (uvt == 1 && M.tex >= 0) cnt.tex++;
           }
-          {
-            V3 ray_col;
-            const float roughness = M.roughness;
-            if (M.model == DT_MODEL_OREN_NAYAR) {
-              float A = (float)(1.0 - (0.5 * pw2((double)roughness)) / (pw2((double)roughness) + 0.33));
-              float B = (float)((0.45 * pw2((double)roughness)) / (pw2((double)roughness) + 0.09));
-              float vn = (float)dot(e_dir, normal);
-              float ln = (float)dot(sn, normal);
-              float irradiance = fmaxr(0.0f, ln);
-              float vn_theta = acosf(vn), ln_theta = acosf(ln);
-              float angleDiff = (float)dmax(0.0, dot(normalized(sub(e_dir, mul(vn, normal))),
-                                                     normalized(sub(sray, mul(ln, normal)))));
-              float alpha = fmaxr(vn_theta, ln_theta), beta = fminr(vn_theta, ln_theta);
-              float f = A + B * angleDiff * sinf(alpha) * tanf(beta);
-              ray_col = mul(f, mul(irradiance, cwise(shape_color, lc)));
-            } else if (M.model == DT_MODEL_COOK_TORRANCE) {
-              V3 H = normalized(add(e_dir, sray));
-              float hn = (float)dmax(0.0, dot(normal, H));
-              float vh = (float)dot(e_dir, H);
-              float vn = (float)dot(e_dir, normal);
-              float ln = (float)dot(sn, normal);
-              float alpha = acosf(hn);
-              float D = (float)(1 / (pw2((double)roughness) * pw4((double)cosf(alpha))) *
-                                exp(-pw2((double)(tanf(alpha) / roughness))));
-              float G1 = (float)(2.0 * hn * vn / vh);
-              float G2 = (float)(2.0 * hn * ln / vh);
-              float G = 1.0f;
-              if (G1 < G) G = G1;
-              if (G2 < G) G = G2;
-              float F = schlick_complex(vn, M.refr[0], M.refr[1]);
-              float fdg = F * D * G;
-              double den = (double)(ln * vn) * M_PI;
-              V3 shader_rgb = add(mul(fmaxr(0.0f, ln), mul(0.4, lc)), divs(mul(fdg, mul(0.8, lc)), den));
-              ray_col = cwise(shape_color, shader_rgb);
-            } else if (M.model == DT_MODEL_RAW) {
-              ray_col = shape_color;
-            } else {
-              V3 r = normalized(add(mul(-1, sray), mul(2 * dot(normal, sray), normal)));
-              double m1 = dmax(0.0, dot(normal, sn));
-              double pp = pw_rt(dmax(0.0, dot(r, e_dir)), (double)P.phong);
-              V3 shader_rgb = add(mul(m1, lc), mul(pp, lc));
-              ray_col = cwise(shape_color, shader_rgb);
-            }
-            if (!is_approx_zero(ray_col)) {
-              hits++;
-              tmp_color = add(tmp_color, mul(k, ray_col));
-            }
+          V3 ray_col;
+          const float roughness = M.roughness;
+          if (M.model == DT_MODEL_OREN_NAYAR) {
+            float A = (float)(1.0 - (0.5 * pw2((double)roughness)) / (pw2((double)roughness) + 0.33));
+            float B = (float)((0.45 * pw2((double)roughness)) / (pw2((double)roughness) + 0.09));
+            float vn = (float)dot(e_dir, normal);
+            float ln = (float)dot(sn, normal);
+            float irradiance = fmaxr(0.0f, ln);
+            float vn_theta = acosf(vn), ln_theta = acosf(ln);
+            float angleDiff = (float)dmax(0.0, dot(normalized(sub(e_dir, mul(vn, normal))),
+                                                   normalized(sub(sray, mul(ln, normal)))));
+            float alpha = fmaxr(vn_theta, ln_theta), beta = fminr(vn_theta, ln_theta);
+            float f = A + B * angleDiff * sinf(alpha) * tanf(beta);
+            ray_col = mul(f, mul(irradiance, cwise(shape_color, lc)));
+          } else if (M.model == DT_MODEL_COOK_TORRANCE) {
+            V3 H = normalized(add(e_dir, sray));
+            float hn = (float)dmax(0.0, dot(normal, H));
+            float vh = (float)dot(e_dir, H);
+            float vn = (float)dot(e_dir, normal);
+            float ln = (float)dot(sn, normal);
+            float alpha = acosf(hn);
+            float D = (float)(1 / (pw2((double)roughness) * pw4((double)cosf(alpha))) *
+                              exp(-pw2((double)(tanf(alpha) / roughness))));
+            float G1 = (float)(2.0 * hn * vn / vh);
+            float G2 = (float)(2.0 * hn * ln / vh);
+            float G = 1.0f;
+            if (G1 < G) G = G1;
+            if (G2 < G) G = G2;
+            float F = schlick_complex(vn, M.refr[0], M.refr[1]);
+            float fdg = F * D * G;
+            double den = (double)(ln * vn) * M_PI;
+            V3 shader_rgb = add(mul(fmaxr(0.0f, ln), mul(0.4, lc)), divs(mul(fdg, mul(0.8, lc)), den));
+            ray_col = cwise(shape_color, shader_rgb);
+          } else if (M.model == DT_MODEL_RAW) {
+            ray_col = shape_color;
+          } else {
+            V3 r = normalized(add(mul(-1, sray), mul(2 * dot(normal, sray), normal)));
+            double m1 = dmax(0.0, dot(normal, sn));
+            double pp = pw_rt(dmax(0.0, dot(r, e_dir)), (double)P.phong);
+            V3 shader_rgb = add(mul(m1, lc), mul(pp, lc));
+            ray_col = cwise(shape_color, shader_rgb);
+          }
+          if (!is_approx_zero(ray_col)) {
+            hits++;
+            tmp_color = add(tmp_color, mul(k, ray_col));
           }
         }
+        if (hits > 0) own = divs(tmp_color, hits);
       }
-      if (shade && !aborted && hits > 0) own = divs(tmp_color, hits);
     }
     DT_T(t6);
     DT_ACC(4, t3, t6);
@@ -1505,7 +1518,8 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   const DScene& S = Lp->S;
   const DParams& P = Lp->P;
   __shared__ double red[DT_WAVE * 3];
-  __shared__ float dens[DT_MAX_CLOUD_STEPS];
+  __shared__ float dens[DT_CLOUD_CHUNK];
+  __shared__ double nrec[9][DT_WAVE];   // per-lane shading record across the shadow walks
   __shared__ double chan[4];
   __shared__ unsigned long long item_s;
   Entry stack[DT_STACK_MAX];
@@ -1591,7 +1605,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         po.color = v3(0, 0, 0);
         po.hit = pass > 0;
         po.in_motion = false;
-        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt);
+        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt, nrec);
         if (pass == 0) {
           tmp_color = po.color;
           hit0 = po.hit;
