@@ -21,17 +21,20 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {
-    # name: (xRes, yRes, antialias_samples, max_depth, brdf_samples)
-    "c3": (1920, 1080, 64, 8, 2),
-    "c2": (800, 600, 16, 4, 2),
+    # name: (xRes, yRes, antialias_samples, max_depth, brdf_samples, use_model)
+    "c3": (1920, 1080, 64, 8, 2, 0),
+    "c2": (800, 600, 16, 4, 2, 0),
+    # C4: the full scene incl. the OBJ models (substitute meshes, tools/gen_models.py), 256 spp
+    "c4": (1920, 1080, 256, 8, 2, 1),
 }
 
 
 def build_globals(dt, cfg):
     g = dt.globals_default()
-    g.use_model = 0
+    xres, yres, aa, depth, brdf, models = CONFIGS[cfg]
+    g.use_model = models
     built = dt.build_scene("final", 240, g)
-    g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.brdf_samples = CONFIGS[cfg]
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.brdf_samples = xres, yres, aa, depth, brdf
     return g, built
 
 
@@ -170,10 +173,12 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "reference scene buildFinal(240), no OBJ models (absent, F6)",
+            "data": ("reference scene buildFinal(240) with substitute OBJ models (tools/gen_models.py)"
+                     if g.use_model else "reference scene buildFinal(240), no OBJ models (absent, F6)"),
             "config": {"workload": "buildFinal(240) %dx%d, %d spp, depth %d, brdf_samples %d, DoF aperture 0.2, "
                                    "glossy + Cook-Torrance + 4 area lights" % (W, H, spp, g.max_depth,
                                                                               g.brdf_samples),
+                       "name": args.config, "use_model": int(g.use_model),
                        "frame": 240, "xRes": W, "yRes": H, "spp": spp, "max_depth": g.max_depth,
                        "parallelism": "tile-split x%d + RCCL gather" % world if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 4), "peak": peak, "unit": "GB/s",

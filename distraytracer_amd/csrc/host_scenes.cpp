@@ -278,6 +278,170 @@ int load_texture(OwnedDesc& O, const std::string& data_dir, const std::string& n
   return (int)O.tex.size() - 1;
 }
 
+// Triangle(a, b, c, col, material, in_motion, shader)  geometry.cpp:434-445
+dt_shape_desc Triangle(V3 a, V3 b, V3 c, V3 col, const std::string& material = "", bool motion = false,
+                       const std::string& shader = "lambert")
+{
+  dt_shape_desc s = blank(DT_SHAPE_TRIANGLE);
+  set3(s.v[0], a);
+  set3(s.v[1], b);
+  set3(s.v[2], c);
+  set3(s.color, col);
+  s.material = material_of(material);
+  s.model = model_of(shader);
+  if (motion) s.flags |= DT_F_MOTION;
+  set3(s.center, divs(add(add(a, b), c), 3));
+  return s;
+}
+
+// loadObj (objHelper.h:6-85, tinyobj): positions and texcoords as float (tinyobj real_t),
+// triangle faces "f v[/vt[/vn]] x3" with 1-based indices. Only what finalBuildModels uses.
+struct ObjMesh {
+  std::vector<V3> v;
+  std::vector<double> vt;            // pairs
+  std::vector<int> vi, ti;           // 3 per triangle; ti = -1 without texcoords
+};
+
+bool load_obj(const std::string& path, ObjMesh& m, std::string& err)
+{
+  std::ifstream f(path);
+  if (!f) {
+    err = "TinyObjReader: cannot open " + path;
+    return false;
+  }
+  std::string line;
+  while (std::getline(f, line)) {
+    if (line.size() < 2 || line[0] == '#') continue;
+    const char* c = line.c_str();
+    if (c[0] == 'v' && c[1] == ' ') {
+      float x, y, z;
+      if (sscanf(c + 2, "%f %f %f", &x, &y, &z) != 3) { err = "bad vertex: " + line; return false; }
+      m.v.push_back(v3(x, y, z));
+    } else if (c[0] == 'v' && c[1] == 't') {
+      float u, w;
+      if (sscanf(c + 3, "%f %f", &u, &w) != 2) { err = "bad texcoord: " + line; return false; }
+      m.vt.push_back(u);
+      m.vt.push_back(w);
+    } else if (c[0] == 'f' && c[1] == ' ') {
+      const char* q = c + 2;
+      int got = 0;
+      while (*q && got < 3) {
+        while (*q == ' ') ++q;
+        if (!*q) break;
+        int vi = 0, ti = 0;
+        int n = 0;
+        if (sscanf(q, "%d/%d%n", &vi, &ti, &n) == 2) {
+        } else if (sscanf(q, "%d%n", &vi, &n) == 1) {
+          ti = 0;
+        } else {
+          err = "bad face: " + line;
+          return false;
+        }
+        q += n;
+        while (*q && *q != ' ') ++q;   // skip a trailing /vn
+        m.vi.push_back(vi - 1);
+        m.ti.push_back(ti - 1);
+        ++got;
+      }
+      if (got != 3) { err = "non-triangle face: " + line; return false; }
+    }
+  }
+  for (int i : m.vi)
+    if (i < 0 || i >= (int)m.v.size()) { err = "vertex index out of range in " + path; return false; }
+  for (int i : m.ti)
+    if (i >= (int)(m.vt.size() / 2)) { err = "texcoord index out of range in " + path; return false; }
+  return true;
+}
+
+// MATRIX4 * (p, 1), head<3>: sequential sums over k (Eigen fixed-size product)
+V3 xform(const double M[3][4], V3 p)
+{
+  double o[3];
+  for (int i = 0; i < 3; ++i) o[i] = ((M[i][0] * p.x + M[i][1] * p.y) + M[i][2] * p.z) + M[i][3] * 1.0;
+  return v3(o[0], o[1], o[2]);
+}
+
+// finalBuildModels (scene.h:258-602) with the substitute assets of tools/gen_models.py
+int final_build_models(dt_globals& g, const std::string& data_dir, OwnedDesc& O, std::string& err)
+{
+  const float min_y = (float)(0.301897 + g.tot_move);
+  const std::string mdir = data_dir + "/models/";
+  ObjMesh col;
+  if (!load_obj(mdir + "Column_LP_obj/Column_LP.obj", col, err)) return DT_E_IO;
+  // loadTexture(Marble_Base_Color) then the roughness map read raw with stbi_load
+  std::vector<uint8_t> tex, rough;
+  int tw, th, tn, rw, rh, rn;
+  if (!load_rgb(mdir + "Column_LP_obj/Textures/Marble_Base_Color.jpg.rgb", tex, tw, th, tn) ||
+      !load_rgb(mdir + "Column_LP_obj/Textures/Marble_Roughness.jpg.rgb", rough, rw, rh, rn)) {
+    err = "Image loading failed for: " + mdir + "Column_LP_obj/Textures";
+    return DT_E_IO;
+  }
+  dt_texture_desc td;
+  memset(&td, 0, sizeof(td));
+  td.width = tw;
+  td.height = th;
+  td.channels = tn;
+  O.tex.push_back(td);
+  O.texdata.push_back(std::move(tex));
+  const int tex_index = (int)O.tex.size() - 1;
+  for (int side = 0; side < 2; ++side) {   // left (-3) and right (+3) straddle columns
+    const double M[3][4] = {{3, 0, 0, side ? 3.0 : -3.0}, {0, 3, 0, (double)min_y}, {0, 0, 3, 5}};
+    std::vector<V3> pv(col.v.size());
+    for (size_t i = 0; i < col.v.size(); ++i) pv[i] = xform(M, col.v[i]);
+    for (size_t i = 0; i < col.vi.size() / 3; ++i) {
+      const int* vi = &col.vi[3 * i];
+      const int* ti = &col.ti[3 * i];
+      if (ti[0] < 0 || ti[1] < 0 || ti[2] < 0) { err = "column mesh needs texcoords"; return DT_E_INVALID; }
+      dt_shape_desc s = Triangle(pv[vi[0]], pv[vi[1]], pv[vi[2]], v3(0.75, 0.75, 0.75), "marble", false,
+                                 "oren-nayar");
+      double uv[3][2];
+      for (int k = 0; k < 3; ++k) {
+        uv[k][0] = col.vt[2 * ti[k]];
+        uv[k][1] = col.vt[2 * ti[k] + 1];
+        if (uv[k][0] > 1) uv[k][0] = uv[k][0] - (int)uv[k][0];   // scene.h:338-343
+        if (uv[k][1] > 1) uv[k][1] = uv[k][1] - (int)uv[k][1];
+      }
+      if (!(uv[0][0] >= 0 && uv[0][1] <= 1 && uv[1][0] >= 0 && uv[1][1] <= 1 && uv[2][0] >= 0 && uv[2][1] <= 1)) {
+        err = "Texcoords out of bounds";   // scene.h:346-356 throws
+        return DT_E_INVALID;
+      }
+      for (int k = 0; k < 3; ++k) {
+        s.uv[k][0] = uv[k][0];
+        s.uv[k][1] = 1 - uv[k][1];   // scene.h:359-361
+      }
+      s.flags |= DT_F_UV_VERTS | DT_F_TEXTURE;
+      s.tex_frame = tex_index;
+      // roughness map read as raw bytes at the (unwrapped) texcoords, scene.h:373-376
+      float r[3];
+      for (int k = 0; k < 3; ++k) {
+        double u = col.vt[2 * ti[k]], w = col.vt[2 * ti[k] + 1];
+        long idx = (long)(u * (int)(rw - 1) + w * (int)(rh - 1) * (rw - 1));
+        if (idx < 0 || idx >= (long)rough.size()) { err = "roughness index out of range"; return DT_E_INVALID; }
+        r[k] = rough[(size_t)idx];
+      }
+      s.roughness = (r[0] + r[1] + r[2]) / (3 * 255);
+      O.shapes.push_back(s);
+    }
+  }
+  ObjMesh bust;
+  if (!load_obj(mdir + "helios_statue/helios_20.obj", bust, err)) return DT_E_IO;
+  for (int side = 0; side < 2; ++side) {   // scene.h:471-478, 517-521
+    const double M[3][4] = {{1.8 * cos(M_PI), 0, 1.8 * sin(M_PI), side ? 3.0 : -3.0},
+                            {0, 1.8, 0, 3.9 + min_y},
+                            {-1.8 * sin(M_PI), 0, 1.8 * cos(M_PI), 4}};
+    std::vector<V3> hv(bust.v.size());
+    for (size_t i = 0; i < bust.v.size(); ++i) hv[i] = xform(M, bust.v[i]);
+    for (size_t i = 2; i < bust.vi.size() / 3; ++i) {   // the reference starts at triangle 2
+      const int* vi = &bust.vi[3 * i];
+      dt_shape_desc s = Triangle(hv[vi[0]], hv[vi[1]], hv[vi[2]], v3(0.75, 0.75, 0.75), "marble", false,
+                                 "oren-nayar");
+      s.roughness = 0.5f;
+      O.shapes.push_back(s);
+    }
+  }
+  return DT_OK;
+}
+
 // ---- buildSceneSpheres (scene.h:4399-4420) --------------------------------------------
 int build_spheres(float frame, dt_globals& g, OwnedDesc& O)
 {
@@ -590,9 +754,9 @@ int build_final(float frame, dt_globals& g, const std::string& data_dir, OwnedDe
       length_vector = normalized(sub(sb, sa));
       theta = (float)acos(1 - pow(w_prism, 2) / pow(norm(sub(sa, tmp_center)), 2));
     }
-    if (g.use_model && frame < g.frame_prism) {
-      err = "buildFinal with use_model needs ./models (absent, SURVEY F6): set use_model = 0";
-      return DT_E_UNSUPPORTED;
+    if (g.use_model && frame < g.frame_prism) {   // scene.h:1095-1098 (substitute assets, F6)
+      int rc = final_build_models(g, data_dir, O, err);
+      if (rc) return rc;
     }
   }
   return DT_OK;

@@ -78,8 +78,8 @@ def test_errors_are_status_codes():
     g = dt.globals_default()
     with pytest.raises(dt.DTError, match="unknown scene"):
         dt.build_scene("nope", 0, g)
-    with pytest.raises(dt.DTError, match="use_model"):
-        dt.build_scene("final", 240, dt.globals_default())   # models absent (F6)
+    with pytest.raises(dt.DTError, match=r"failed \(-5\)"):
+        dt.build_scene("final", 240, dt.globals_default(), data_dir="/nonexistent")   # DT_E_IO
     bad = _lib.SceneDesc()
     bad.n_shapes = -1
     h = ctypes.c_void_p()

@@ -115,6 +115,25 @@ def test_final_c2_windows(cuda, window):
     _cmp(gpu[m], ref[m], 0.002, "final C2 %s" % (window,))
 
 
+def test_final_models_window(cuda):
+    """buildFinal(480) with use_model=true (substitute column/bust meshes, tools/gen_models.py):
+    ~2400 UV-mapped triangles, textured Oren-Nayar marble, roughness from the map; the window
+    covers a column and its bust."""
+    g = dt.globals_default()
+    g.use_model = 1
+    built = dt.build_scene("final", 480, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.brdf_samples = 320, 180, 16, 4, 2
+    x0, y0, x1, y1 = 24, 20, 72, 100
+    tile = dt.tiles(x0=x0, y0=y0, x1=x1, y1=y1)
+    gpu, st = _render_gpu(built, g, 480, tile)
+    ref, _ = oracle.render(built, g, 480, tile)
+    m = np.zeros((180, 320), dtype=bool)
+    m[180 - y1:180 - y0, x0:x1] = True
+    m = np.repeat(m.reshape(-1), 3)
+    assert st.tex_fetches > 0
+    _cmp(gpu[m], ref[m], 0.002, "final models window")
+
+
 def test_final_c3_window(cuda):
     """C3 settings (1920x1080, 64 spp, depth 8) on a window around the window/sky region."""
     g = dt.globals_default()

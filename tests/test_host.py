@@ -49,11 +49,29 @@ def test_build_spheres_matches_reference_constants():
     assert list(d.lights[0].center) == [-6, 0.5, 1]
 
 
-@pytest.mark.parametrize("name,frame", [("final", 240), ("spheres", 0), ("dof", 0), ("hw4", 0),
-                                        ("final", 0), ("final", 480), ("final", 2000)])
-def test_bvh_topology_equals_oracle(name, frame):
+def test_build_final_models_inventory():
+    """use_model=true: finalBuildModels (scene.h:258-602) adds two textured columns and two
+    busts from the substitute OBJs (tools/gen_models.py): 2 x 832 + 2 x (364 - 2) triangles,
+    Oren-Nayar marble, per-vertex UVs flipped in v, roughness from the map."""
     g = dt.globals_default()
-    g.use_model = 0
+    g.use_model = 1
+    b = dt.build_scene("final", 240, g)   # keep the owner alive while reading its desc
+    d = b.desc
+    tris = [d.shapes[i] for i in range(d.n_shapes) if d.shapes[i].type == 3]
+    assert len(tris) == 2 * 832 + 2 * 362 and d.n_textures == 4
+    col, bust = tris[:2 * 832], tris[2 * 832:]
+    assert all(t.model == 1 and t.flags & 4 and t.flags & 64 and t.tex_frame == 3 for t in col)
+    assert all(0 <= t.uv[k][j] <= 1 for t in col for k in range(3) for j in range(2))
+    assert all(0.2 < t.roughness < 0.8 for t in col)
+    assert all(t.roughness == 0.5 and not t.flags & 4 for t in bust)
+
+
+@pytest.mark.parametrize("name,frame,models", [("final", 240, 0), ("spheres", 0, 0), ("dof", 0, 0), ("hw4", 0, 0),
+                                               ("final", 0, 0), ("final", 480, 0), ("final", 2000, 0),
+                                               ("final", 480, 1)])
+def test_bvh_topology_equals_oracle(name, frame, models):
+    g = dt.globals_default()
+    g.use_model = models
     b = dt.build_scene(name, frame, g)
     scene_nodes, scene_idx = _device_free_bvh(b, g)
     or_nodes, or_idx = oracle.bvh(b, g)
