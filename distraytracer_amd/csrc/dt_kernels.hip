@@ -120,6 +120,16 @@ __device__ __forceinline__ double pw_rt(double x, double y)
   return pow(x, y);
 }
 
+// The reference's float libm calls (cosf/sinf/tanf/acosf through <cmath>'s float overloads)
+// are evaluated correctly rounded, as f32(f64 function): the reference's float libm is
+// platform dependent (glibc's cosf is not correctly rounded either) and its float quadratic
+// solves amplify a 1-ulp difference in a DoF offset into ~30 ulp of a hit distance. The oracle
+// uses the same definition (oracle.c cr_cosf...), so both sides agree bit for bit.
+__device__ __forceinline__ float cr_cosf(float x) { return (float)cos((double)x); }
+__device__ __forceinline__ float cr_sinf(float x) { return (float)sin((double)x); }
+__device__ __forceinline__ float cr_tanf(float x) { return (float)tan((double)x); }
+__device__ __forceinline__ float cr_acosf(float x) { return (float)acos((double)x); }
+
 // =====================================================================================
 // value noise (noise.h:25-136) and sky (render_final_project.cpp:146-192)
 // =====================================================================================
@@ -1418,11 +1428,11 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
             float vn = (float)dot(e_dir, normal);
             float ln = (float)dot(sn, normal);
             float irradiance = fmaxr(0.0f, ln);
-            float vn_theta = acosf(vn), ln_theta = acosf(ln);
+            float vn_theta = cr_acosf(vn), ln_theta = cr_acosf(ln);
             float angleDiff = (float)dmax(0.0, dot(normalized(sub(e_dir, mul(vn, normal))),
                                                    normalized(sub(sray, mul(ln, normal)))));
             float alpha = fmaxr(vn_theta, ln_theta), beta = fminr(vn_theta, ln_theta);
-            float f = A + B * angleDiff * sinf(alpha) * tanf(beta);
+            float f = A + B * angleDiff * cr_sinf(alpha) * cr_tanf(beta);
             ray_col = mul(f, mul(irradiance, cwise(shape_color, lc)));
           } else if (M.model == DT_MODEL_COOK_TORRANCE) {
             V3 H = normalized(add(e_dir, sray));
@@ -1430,9 +1440,9 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
             float vh = (float)dot(e_dir, H);
             float vn = (float)dot(e_dir, normal);
             float ln = (float)dot(sn, normal);
-            float alpha = acosf(hn);
-            float D = (float)(1 / (pw2((double)roughness) * pw4((double)cosf(alpha))) *
-                              exp(-pw2((double)(tanf(alpha) / roughness))));
+            float alpha = cr_acosf(hn);
+            float D = (float)(1 / (pw2((double)roughness) * pw4((double)cr_cosf(alpha))) *
+                              exp(-pw2((double)(cr_tanf(alpha) / roughness))));
             float G1 = (float)(2.0 * hn * vn / vh);
             float G2 = (float)(2.0 * hn * ln / vh);
             float G = 1.0f;
@@ -1569,7 +1579,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         c.rng.draw(0, P_DOF, 0, u0, u1);
         float r = (float)(P.aperture / 2 * u0);
         float theta = (float)(2 * M_PI * u1);
-        eye_sample = add(add(eye, mul(r * cosf(theta), X)), mul(r * sinf(theta), Y));
+        eye_sample = add(add(eye, mul(r * cr_cosf(theta), X)), mul(r * cr_sinf(theta), Y));
       }
       float a = P.l + (P.r - P.l) * (float)px_x / (float)P.xRes;
       float b = P.b + (P.t - P.b) * (float)px_y / (float)P.yRes;

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <fstream>
 #include <memory>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -442,6 +443,110 @@ int final_build_models(dt_globals& g, const std::string& data_dir, OwnedDesc& O,
   return DT_OK;
 }
 
+// ---- ./ads substitute --------------------------------------------------------
+// The reference lists every ./ads/<campaign>/*.jpg into frame_paths (render_final_project.cpp:
+// 90-95, 1401-1406) and the tunnel mesh picks frames from it. The assets are absent; the
+// substitute is a fixed-size list of procedurally generated 80x45 "ad" frames, frame i being
+// a deterministic function of i (a banner colour, stripes and blocks), generated on load.
+const int kAdFrames = 2400;   // >= 1000 + (frame_cloud - frame_prism): every index stays in range
+const int kAdW = 80, kAdH = 45;
+
+uint32_t ad_hash(uint32_t x)
+{
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+
+int load_ad_frame(OwnedDesc& O, int idx)
+{
+  std::vector<uint8_t> px((size_t)kAdW * kAdH * 3);
+  const uint32_t h0 = ad_hash((uint32_t)idx * 2654435761u + 17u);
+  const int br = 60 + (h0 & 127), bg = 60 + ((h0 >> 7) & 127), bb = 60 + ((h0 >> 14) & 127);
+  const int stripe = 3 + ((h0 >> 21) & 7);
+  for (int y = 0; y < kAdH; ++y)
+    for (int x = 0; x < kAdW; ++x) {
+      uint8_t* q = &px[((size_t)y * kAdW + x) * 3];
+      const bool band = ((x + y + idx) / stripe) % 3 == 0;
+      const bool block = x > 10 && x < 40 && y > 12 && y < 32;
+      q[0] = (uint8_t)(block ? 255 - br : band ? br / 2 : br);
+      q[1] = (uint8_t)(block ? 255 - bg : band ? bg / 2 : bg);
+      q[2] = (uint8_t)(block ? 255 - bb : band ? bb / 2 : bb);
+    }
+  dt_texture_desc t;
+  memset(&t, 0, sizeof(t));
+  t.width = kAdW;
+  t.height = kAdH;
+  t.channels = 3;
+  O.tex.push_back(t);
+  O.texdata.push_back(std::move(px));
+  return (int)O.tex.size() - 1;
+}
+
+// generateTrianglePrismMesh (scene.h:135-256): the ad-covered tunnel the camera falls through
+void triangle_prism_mesh(OwnedDesc& O, const dt_globals& g, V3 a_cap0, V3 b_cap0, V3 c_cap0, V3 a_cap1, V3 b_cap1,
+                         V3 c_cap1, int time_frame, bool texture, bool motion)
+{
+  static std::mt19937 gen(0);   // scene.h:57, reseeded per rectangle
+  std::uniform_int_distribution<> unif(0, kAdFrames - 1000);
+  const V3 eye = v3a(g.eye);
+  const float far = g.far_dist;
+  O.shapes.push_back(Triangle(a_cap1, b_cap1, c_cap1, v3(1, 1, 1)));
+  const int n_rect = 4;
+  const float bounding_width = 0.1f;
+  const float rect_height = (float)((norm(sub(a_cap0, b_cap0)) - bounding_width * n_rect) / n_rect);
+  const float rect_width = (float)5 / 3 * rect_height;
+  const V3 length_v = normalized(sub(c_cap1, c_cap0));
+  const V3 ac_v = normalized(sub(a_cap0, c_cap0));
+  const V3 ab_v = normalized(sub(a_cap0, b_cap0));
+  const V3 bc_v = normalized(sub(c_cap0, b_cap0));
+  V3 left_a = add(b_cap0, mul(bounding_width, length_v));
+  V3 left_b = add(left_a, mul(rect_width, length_v));
+  V3 left_c = add(left_b, mul(rect_height, ab_v));
+  V3 left_d = add(left_a, mul(rect_height, ab_v));
+  V3 right_b = add(c_cap0, mul(bounding_width, length_v));
+  V3 right_a = add(right_b, mul(rect_width, length_v));
+  V3 right_d = add(right_a, mul(rect_height, ac_v));
+  V3 right_c = add(right_b, mul(rect_height, ac_v));
+  V3 bottom_a = add(add(b_cap0, mul(bounding_width, length_v)), mul(bounding_width, bc_v));
+  V3 bottom_b = add(bottom_a, mul(rect_width, length_v));
+  V3 bottom_c = add(bottom_b, mul(rect_height, bc_v));
+  V3 bottom_d = add(bottom_a, mul(rect_height, bc_v));
+  const V3 adj_b0 = add(b_cap0, divs(mul(bounding_width, bc_v), 2));
+  int seed_counter = 0;
+  auto place = [&](V3 a, V3 b, V3 c, V3 d, V3 dir, int i, uint32_t seed) {
+    gen.seed(seed);
+    const int frame_ind = unif(gen) + (time_frame - g.frame_prism);
+    const int tex_index = load_ad_frame(O, frame_ind);
+    const V3 off = mul((double)i, mul(bounding_width + rect_height, dir));
+    dt_shape_desc r = Rectangle(add(a, off), add(b, off), add(c, off), add(d, off), v3(0, 1, 0), "", motion,
+                                tex_index, "raw");
+    if (motion) r.flags |= DT_F_MOTION;
+    if (texture) r.flags |= DT_F_TEXTURE;
+    O.shapes.push_back(r);
+  };
+  while (norm(sub(bottom_b, adj_b0)) <= norm(sub(c_cap1, c_cap0))) {
+    for (int i = 0; i < n_rect; i++) {
+      // skip rectangles behind the eye or beyond `far` (scene.h:187-188)
+      if (!(left_b.y > eye.y && left_c.y > eye.y) & !(norm(sub(left_b, eye)) > far && norm(sub(left_c, eye)) > far))
+        place(left_a, left_b, left_c, left_d, ab_v, i, (uint32_t)seed_counter);
+      seed_counter++;
+      if (!(right_a.y > eye.y && right_d.y > eye.y) & !(norm(sub(right_a, eye)) > far && norm(sub(right_d, eye)) > far))
+        place(right_a, right_b, right_c, right_d, ac_v, i, (uint32_t)(seed_counter + 1));
+      seed_counter++;
+      if (!(bottom_b.y > eye.y && bottom_c.y > eye.y) &
+          !(norm(sub(bottom_b, eye)) > far && norm(sub(bottom_c, eye)) > far))
+        place(bottom_a, bottom_b, bottom_c, bottom_d, bc_v, i, (uint32_t)(seed_counter + 2));
+      seed_counter++;
+    }
+    const V3 step = mul(rect_width + bounding_width, length_v);
+    left_a = add(left_a, step); left_b = add(left_b, step); left_c = add(left_c, step); left_d = add(left_d, step);
+    right_a = add(right_a, step); right_b = add(right_b, step); right_c = add(right_c, step);
+    right_d = add(right_d, step);
+    bottom_a = add(bottom_a, step); bottom_b = add(bottom_b, step); bottom_c = add(bottom_c, step);
+    bottom_d = add(bottom_d, step);
+  }
+}
+
 // ---- buildSceneSpheres (scene.h:4399-4420) --------------------------------------------
 int build_spheres(float frame, dt_globals& g, OwnedDesc& O)
 {
@@ -622,9 +727,24 @@ int build_final(float frame, dt_globals& g, const std::string& data_dir, OwnedDe
     lerp(g.sun_core, darkblue);
     return DT_OK;
   }
-  if (frame >= g.frame_prism) {
-    err = "buildFinal frames >= frame_prism need the ./ads textures (absent, SURVEY F6)";
-    return DT_E_UNSUPPORTED;
+  // the tunnel (scene.h:776-781, 806-871): caps scaled x5 about their centre, pulled up by
+  // the movement, rotated about +y, extruded 263 down; ads from the substitute frame list
+  {
+    const float dist = 263;
+    a_cap0 = add(mul(5, sub(a_cap0, cap_center)), cap_center);
+    b_cap0 = add(mul(5, sub(b_cap0, cap_center)), cap_center);
+    c_cap0 = add(mul(5, sub(c_cap0, cap_center)), cap_center);
+    a_cap0 = add(a_cap0, v3(0, g.tot_move, 0));
+    b_cap0 = add(b_cap0, v3(0, g.tot_move, 0));
+    c_cap0 = add(c_cap0, v3(0, g.tot_move, 0));
+    const float rot_theta = (float)(movement_multiplier / 720.0 * M_PI);
+    a_cap0 = add(rotate(sub(a_cap0, cap_center), v3(0, 1, 0), rot_theta), cap_center);
+    b_cap0 = add(rotate(sub(b_cap0, cap_center), v3(0, 1, 0), rot_theta), cap_center);
+    c_cap0 = add(rotate(sub(c_cap0, cap_center), v3(0, 1, 0), rot_theta), cap_center);
+    const V3 a_cap1 = sub(a_cap0, v3(0, dist, 0)), b_cap1 = sub(b_cap0, v3(0, dist, 0)),
+             c_cap1 = sub(c_cap0, v3(0, dist, 0));
+    if (frame >= g.frame_prism)
+      triangle_prism_mesh(O, g, a_cap0, b_cap0, c_cap0, a_cap1, b_cap1, c_cap1, (int)frame, true, true);
   }
   if ((min_y + g.tot_move <= eye.y + 2) || frame < g.frame_prism + tunnel_transition) {
     float angle = (float)(fminr(1.1f, movement_multiplier / (tunnel_transition)) * M_PI / 2);

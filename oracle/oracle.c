@@ -33,6 +33,13 @@
 #define M_PI 3.14159265358979323846
 #endif
 
+/* float libm calls evaluated correctly rounded, f32(f64 function) — the definition the
+ * device uses too (dt_kernels.hip cr_cosf...). */
+static inline float cr_cosf(float x) { return (float)cos((double)x); }
+static inline float cr_sinf(float x) { return (float)sin((double)x); }
+static inline float cr_tanf(float x) { return (float)tan((double)x); }
+static inline float cr_acosf(float x) { return (float)acos((double)x); }
+
 /* ======================================================================= */
 /* vector helpers (Eigen semantics, header comment)                         */
 /* ======================================================================= */
@@ -1418,13 +1425,13 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
         float vn = (float)dot(e, normal);
         float ln = (float)dot(sn, normal);
         float irradiance = fmaxr(0.0f, ln);
-        float vn_theta = acosf(vn);
-        float ln_theta = acosf(ln);
+        float vn_theta = cr_acosf(vn);
+        float ln_theta = cr_acosf(ln);
         float angleDiff = (float)dmax(0.0, dot(normalized(sub(e, mul(vn, normal))),
                                                normalized(sub(sray, mul(ln, normal)))));
         float alpha = fmaxr(vn_theta, ln_theta);
         float beta = fminr(vn_theta, ln_theta);
-        float f = A + B * angleDiff * sinf(alpha) * tanf(beta);
+        float f = A + B * angleDiff * cr_sinf(alpha) * cr_tanf(beta);
         V3 sc_lc = v3(shape_color.x * lc.x, shape_color.y * lc.y, shape_color.z * lc.z);
         ray_col = mul(f, mul(irradiance, sc_lc));
       } else if (model == DT_MODEL_COOK_TORRANCE) {  /* 914-938 */
@@ -1433,9 +1440,9 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
         float vh = (float)dot(e, H);
         float vn = (float)dot(e, normal);
         float ln = (float)dot(sn, normal);
-        float alpha = acosf(hn);
-        float D = (float)(1 / (pow(roughness, 2) * pow(cosf(alpha), 4)) *
-                          exp(-pow(tanf(alpha) / roughness, 2)));
+        float alpha = cr_acosf(hn);
+        float D = (float)(1 / (pow(roughness, 2) * pow(cr_cosf(alpha), 4)) *
+                          exp(-pow(cr_tanf(alpha) / roughness, 2)));
         float G1 = (float)(2.0 * hn * vn / vh);
         float G2 = (float)(2.0 * hn * ln / vh);
         float G = 1.0f;                       /* std::min({1, G1, G2}) */
@@ -1640,7 +1647,7 @@ static void render_sample(const RenderCtx* R, const dt_globals* g, int x, int y,
     rng2(&c.rng, 0, P_DOF, 0, &u0, &u1);
     float r = (float)(g->aperture / 2 * u0);
     float theta = (float)(2 * M_PI * u1);
-    eye_sample = add(add(cam->eye, mul(r * cosf(theta), cam->X)), mul(r * sinf(theta), cam->Y));
+    eye_sample = add(add(cam->eye, mul(r * cr_cosf(theta), cam->X)), mul(r * cr_sinf(theta), cam->Y));
   }
   V3 rayDir = persp_eye_ray(g, cam, x, y);
   V3 focalPoint = add(cam->eye, mul(g->focal_length, rayDir));

@@ -1,10 +1,12 @@
 """GPU parity: libdt's HIP kernels vs the CPU oracle on identical inputs and seeds.
 
 Tolerance (north_star): 1e-4 per channel on the float ppmOut values. The device repeats the
-reference's operation sequence in IEEE FP64/FP32 without contraction, so most pixels agree
-bit for bit; the remaining differences come from OCML vs glibc transcendentals (<= 1 ulp)
-flipping a threshold test (t <= eps, u < 0, ...). Each test therefore bounds the FRACTION of
-channels outside 1e-4, with the bound written next to it.
+reference's operation sequence in IEEE FP64/FP32 without contraction, and evaluates the
+reference's float libm calls (cosf/sinf/tanf/acosf) correctly rounded on both sides
+(DESIGN.md §5), so every case below is bit-identical today (max|diff| = 0). Each test still
+bounds only the FRACTION of channels outside 1e-4 (written next to it), leaving room for a
+1-ulp OCML-vs-glibc difference in an f64 transcendental that the reference's float quadratic
+solves can amplify at a silhouette.
 """
 import numpy as np
 import pytest
@@ -132,6 +134,27 @@ def test_final_models_window(cuda):
     m = np.repeat(m.reshape(-1), 3)
     assert st.tex_fetches > 0
     _cmp(gpu[m], ref[m], 0.002, "final models window")
+
+
+@pytest.mark.parametrize("n", [150, 210])
+def test_final_c5_tunnel_motion_blur(cuda, n):
+    """C5 animation frames buildFinal(n*8) (scene.h:605-1100): the ad tunnel (substitute ./ads
+    frames, generateTrianglePrismMesh) with every "rectangle" in motion. Frame 1200 blurs with
+    the linear shift, frame 1680 (>= frame_blur) with the cubic acceleration term; both shift
+    the tunnel rectangles and bump the BVH leaves (general traversal path)."""
+    g = dt.globals_default()
+    g.use_model = 0
+    built = dt.build_scene("final", n * 8, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = 320, 180, 4, 3
+    x0, y0, x1, y1 = 128, 60, 192, 108
+    tile = dt.tiles(x0=x0, y0=y0, x1=x1, y1=y1)
+    gpu, st = _render_gpu(built, g, n * 8, tile)
+    ref, rst = oracle.render(built, g, n * 8, tile)
+    m = np.zeros((180, 320), dtype=bool)
+    m[180 - y1:180 - y0, x0:x1] = True
+    m = np.repeat(m.reshape(-1), 3)
+    assert st.rays > st.samples and st.rays == rst.rays   # blur re-traces, same count as the oracle
+    _cmp(gpu[m], ref[m], 0.003, "final C5 frame %d" % (n * 8))
 
 
 def test_final_c3_window(cuda):

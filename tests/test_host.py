@@ -66,9 +66,24 @@ def test_build_final_models_inventory():
     assert all(t.roughness == 0.5 and not t.flags & 4 for t in bust)
 
 
+def test_build_final_tunnel_frames():
+    """frames >= frame_prism (C5): generateTrianglePrismMesh (scene.h:135-256) adds the bottom
+    cap triangle and the ad rectangles (substitute ./ads frames), all in motion and named
+    "rectangle", each with its own texture; the doors/room are gone once the eye passed them."""
+    g = dt.globals_default()
+    g.use_model = 0
+    b = dt.build_scene("final", 1200, g)
+    d = b.desc
+    rects = [d.shapes[i] for i in range(d.n_shapes) if d.shapes[i].type == 4]
+    assert len(rects) == d.n_textures > 500
+    assert all(r.flags & 2 and r.flags & 4 and r.flags & 16 and r.model == 3 for r in rects)
+    assert sum(d.shapes[i].type == 3 for i in range(d.n_shapes)) == 1
+    assert g.focal_length == 20 and list(g.up) == [0, 0, -1]
+
+
 @pytest.mark.parametrize("name,frame,models", [("final", 240, 0), ("spheres", 0, 0), ("dof", 0, 0), ("hw4", 0, 0),
                                                ("final", 0, 0), ("final", 480, 0), ("final", 2000, 0),
-                                               ("final", 480, 1)])
+                                               ("final", 480, 1), ("final", 1200, 0), ("final", 1680, 0)])
 def test_bvh_topology_equals_oracle(name, frame, models):
     g = dt.globals_default()
     g.use_model = models
