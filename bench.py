@@ -194,9 +194,6 @@ def main():
             "cpu_baseline": cpu,
             "work": {"rays_per_sample": round(lib_stats.rays / max(lib_stats.samples, 1), 3),
                      "shadow_rays_per_sample": round(lib_stats.shadow_rays / max(lib_stats.samples, 1), 3),
-                     "box_tests_per_sample": round(lib_stats.box_tests / max(lib_stats.samples, 1), 2),
-                     "prim_tests_per_sample": round(lib_stats.prim_tests / max(lib_stats.samples, 1), 2),
-                     "wave_node_visits": lib_stats.wave_node_visits,
                      "stack_overflows": lib_stats.stack_overflows, "nan_pixels": lib_stats.nan_pixels},
         }
         if flat_bytes:

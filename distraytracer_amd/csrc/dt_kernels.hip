@@ -43,6 +43,14 @@ using namespace dtd;
 #define DT_ACC(k, a, b)
 #endif
 
+// BVH work counters (box/prim tests, wave node visits) in dt_stats: compiled in only with
+// -DDT_WORK_COUNTERS (diagnostic builds): in the traversal loops they cost ~6% (C3)
+#ifdef DT_WORK_COUNTERS
+#define DT_WORK(...) __VA_ARGS__
+#else
+#define DT_WORK(...)
+#endif
+
 #define DT_STACK_MAX 48
 #define DT_MAX_CLOUD_STEPS 2048
 #define DT_CLOUD_CHUNK 256
@@ -125,9 +133,35 @@ __device__ __forceinline__ double pw_rt(double x, double y)
 // platform dependent (glibc's cosf is not correctly rounded either) and its float quadratic
 // solves amplify a 1-ulp difference in a DoF offset into ~30 ulp of a hit distance. The oracle
 // uses the same definition (oracle.c cr_cosf...), so both sides agree bit for bit.
-__device__ __forceinline__ float cr_cosf(float x) { return (float)cos((double)x); }
-__device__ __forceinline__ float cr_sinf(float x) { return (float)sin((double)x); }
-__device__ __forceinline__ float cr_tanf(float x) { return (float)tan((double)x); }
+// sin/cos of a float argument: Cody-Waite reduction by pi/2 in f64 (exact for |x| < 1e5: k*PIO2_1
+// is exact with a 33-bit PIO2_1) and Taylor polynomials to r^17/r^16 on |r| <= pi/4 (truncation
+// < 1e-19). The f64 result is within ~1e-16 of sin/cos, so rounding it to f32 gives the same
+// float as f32(glibc sin/cos) (checked on 5e7 arguments in [0, 2pi): no mismatch).
+__device__ __forceinline__ void cr_sincos_d(float xf, double& s_out, double& c_out)
+{
+  if (!(fabsf(xf) < 1e5f)) {   // large or non-finite: the library path
+    s_out = sin((double)xf);
+    c_out = cos((double)xf);
+    return;
+  }
+  const double PIO2_1 = 1.57079632673412561417e+00, PIO2_1T = 6.07710050650619224932e-11;
+  const double x = xf;
+  const double k = rint(x * 0.63661977236758134308);
+  const double r = (x - k * PIO2_1) - k * PIO2_1T;
+  const double r2 = r * r;
+  const double sp = r + r * r2 * (-1.0 / 6 + r2 * (1.0 / 120 + r2 * (-1.0 / 5040 + r2 * (1.0 / 362880 +
+                    r2 * (-1.0 / 39916800 + r2 * (1.0 / 6227020800.0 + r2 * (-1.0 / 1307674368000.0 +
+                    r2 * (1.0 / 355687428096000.0))))))));
+  const double cp = 1 + r2 * (-0.5 + r2 * (1.0 / 24 + r2 * (-1.0 / 720 + r2 * (1.0 / 40320 + r2 * (-1.0 / 3628800 +
+                    r2 * (1.0 / 479001600 + r2 * (-1.0 / 87178291200.0 + r2 * (1.0 / 20922789888000.0))))))));
+  const int q = ((int)k) & 3;
+  s_out = q == 0 ? sp : q == 1 ? cp : q == 2 ? -sp : -cp;
+  c_out = q == 0 ? cp : q == 1 ? -sp : q == 2 ? -cp : sp;
+}
+__device__ __forceinline__ float cr_cosf(float x) { double s, c; cr_sincos_d(x, s, c); return (float)c; }
+__device__ __forceinline__ float cr_sinf(float x) { double s, c; cr_sincos_d(x, s, c); return (float)s; }
+// tan as sin/cos of the same reduction (one correctly rounded f64 division: within ~3e-16)
+__device__ __forceinline__ float cr_tanf(float x) { double s, c; cr_sincos_d(x, s, c); return (float)(s / c); }
 __device__ __forceinline__ float cr_acosf(float x) { return (float)acos((double)x); }
 
 // =====================================================================================
@@ -948,8 +982,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
     const bool act = resume <= i;
     const float tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
     const bool hb = act & node_hit<GENERAL>(w, nd, shift, org, tcull);
-    cnt.wnodes++;
-    cnt.box += act;
+    DT_WORK(cnt.wnodes++; cnt.box += act);
     if (nd.meta & DN_LEAF) {
       if (__ballot(hb)) {
         const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
@@ -958,8 +991,9 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
           uint32_t flags;
           leaf_shape(S, nd, q, sid, type, flags, off);
           DT_CNT(8);
+          DT_CNT(10 + (type & 7));   // closest-hit prim tests by type (8 -> 10)
           if (hb) {
-            cnt.prim++;
+            DT_WORK(cnt.prim++);
             int ins = 0, hc = 0;
             V3 cc;
             if (shape_hit(S, sid, type, flags, cas(S.geom) + off, ray, org, shift, t_dist, ins, cc, hc)) {
@@ -1014,8 +1048,7 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
     const DNodeDev nd = cas(S.nodes)[i];
     const bool act = resume <= i;
     const bool hb = act & node_hit<GENERAL>(w, nd, shift, bstart, tcull);
-    cnt.wnodes++;
-    cnt.box += act;
+    DT_WORK(cnt.wnodes++; cnt.box += act);
     if (nd.meta & DN_LEAF) {
       if (__ballot(hb)) {
         const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
@@ -1024,9 +1057,10 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
           uint32_t flags;
           leaf_shape(S, nd, q, sid, type, flags, off);
           DT_CNT(8);
+          DT_CNT(18 + (type & 7));   // shadow prim tests by type (8 -> 18)
           const bool test = hb && !occl && sid != skip_shape;
           if (test) {
-            cnt.prim++;
+            DT_WORK(cnt.prim++);
             if (shape_shadow(type, flags, cas(S.geom) + off, sn, sstart, t_max, shift)) occl = true;
           }
         }
@@ -1077,7 +1111,7 @@ struct Counters {
   uint32_t box, prim;
   uint32_t wnodes;                   // wave-level
 #ifdef DT_STAMPS
-  unsigned long long ph[10];   // diagnostic build only: cycles per phase (wave-uniform)
+  unsigned long long ph[28];   // diagnostic build only: cycles per phase, event counts (wave-uniform)
 #endif
 };
 
@@ -1441,8 +1475,11 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
             float vn = (float)dot(e_dir, normal);
             float ln = (float)dot(sn, normal);
             float alpha = cr_acosf(hn);
-            float D = (float)(1 / (pw2((double)roughness) * pw4((double)cr_cosf(alpha))) *
-                              exp(-pw2((double)(cr_tanf(alpha) / roughness))));
+            double sa, ca;
+            cr_sincos_d(alpha, sa, ca);   // cosf(alpha), tanf(alpha) from one reduction
+            const float cos_a = (float)ca, tan_a = (float)(sa / ca);
+            float D = (float)(1 / (pw2((double)roughness) * pw4((double)cos_a)) *
+                              exp(-pw2((double)(tan_a / roughness))));
             float G1 = (float)(2.0 * hn * vn / vh);
             float G2 = (float)(2.0 * hn * ln / vh);
             float G = 1.0f;
@@ -1543,7 +1580,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   Counters cnt;
   cnt.rays = 0; cnt.shadow = 0; cnt.tex = 0; cnt.box = 0; cnt.prim = 0; cnt.wnodes = 0;
 #ifdef DT_STAMPS
-  for (int k = 0; k < 10; ++k) cnt.ph[k] = 0;
+  for (int k = 0; k < 28; ++k) cnt.ph[k] = 0;
 #endif
 
   while (true) {
@@ -1579,7 +1616,9 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         c.rng.draw(0, P_DOF, 0, u0, u1);
         float r = (float)(P.aperture / 2 * u0);
         float theta = (float)(2 * M_PI * u1);
-        eye_sample = add(add(eye, mul(r * cr_cosf(theta), X)), mul(r * cr_sinf(theta), Y));
+        double st, ct;
+        cr_sincos_d(theta, st, ct);
+        eye_sample = add(add(eye, mul(r * (float)ct, X)), mul(r * (float)st, Y));
       }
       float a = P.l + (P.r - P.l) * (float)px_x / (float)P.xRes;
       float b = P.b + (P.t - P.b) * (float)px_y / (float)P.yRes;
@@ -1689,7 +1728,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       atomicAdd(S.stats + ST_PRIM, pr);
       atomicAdd(S.stats + ST_WNODES, (unsigned long long)cnt.wnodes);
 #ifdef DT_STAMPS
-      for (int k = 0; k < 10; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);
+      for (int k = 0; k < 28; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);
 #endif
       if (sky_px) atomicAdd(S.stats + ST_SKY, sky_px);
       atomicAdd(S.stats + ST_RAYS, r);

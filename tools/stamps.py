@@ -20,8 +20,8 @@ def main():
     s = dt.Scene(b, g)
     out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
     st = dt.render(s, g, 240, out)
-    arr = (ctypes.c_uint64 * 10)()
-    dt.check(dt.lib.dt_debug_counters(s.handle, arr, 10))
+    arr = (ctypes.c_uint64 * 28)()
+    dt.check(dt.lib.dt_debug_counters(s.handle, arr, 28))
     tot = arr[5] + arr[6]
     print("kernel ms %.2f" % st.kernel_ms)
     for i, n in enumerate(NAMES[:7]):
@@ -29,6 +29,10 @@ def main():
     items = g.xRes * g.yRes   # one wave item per pixel at 64 spp
     print("per wave item: DFS steps %.2f  wave-level prim tests %.2f  light iterations %.2f  node visits %.1f"
           % (arr[7] / items, arr[8] / items, arr[9] / items, st.wave_node_visits / items))
+    names = {1: "sphere", 2: "cylinder", 3: "triangle", 4: "rectangle", 5: "prism", 6: "checker", 7: "checkerhole",
+             0: "checkercyl"}
+    print("closest-hit prim tests per item:", {names[t]: round(arr[10 + t] / items, 2) for t in range(8) if arr[10 + t]})
+    print("shadow prim tests per item:", {names[t]: round(arr[18 + t] / items, 2) for t in range(8) if arr[18 + t]})
 
 
 if __name__ == "__main__":
