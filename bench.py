@@ -85,7 +85,7 @@ def main():
     import torch.distributed as dist
 
     import distraytracer_amd as dt
-    from distraytracer_amd.multigpu import FrameSplit
+    from distraytracer_amd.multigpu import FrameSplit, GatherPipeline
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -103,28 +103,34 @@ def main():
     if world == 1:
         image = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
         tile = dt.tiles()
-        slab = gathered = None
     else:
-        slab = torch.zeros(split.slab_floats, dtype=torch.float32, device=dev)
-        gathered = torch.zeros(world * split.slab_floats if rank == 0 else 1, dtype=torch.float32, device=dev)
-        image = torch.zeros(3 * W * H if rank == 0 else 1, dtype=torch.float32, device=dev)
+        # double-buffered slabs: frame k's gather (RCCL, async) overlaps frame k+1's render
+        pipe = GatherPipeline(split, [torch.zeros(split.slab_floats, dtype=torch.float32, device=dev)
+                                      for _ in range(2)],
+                              [torch.zeros(world * split.slab_floats if rank == 0 else 1, dtype=torch.float32,
+                                           device=dev) for _ in range(2)],
+                              torch.zeros(3 * W * H if rank == 0 else 1, dtype=torch.float32, device=dev))
         tile = split.tile
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
 
-    def step(evs=None):
+    def finish_pending():
+        if world > 1:
+            pipe.finish()
+
+    def step(k, evs=None):
+        out = image if world == 1 else pipe.slab(k)
         if evs is not None:
             evs[0].record(stream)
-        dt.render_async(scene, g, 240, image if world == 1 else slab, tile, stream=sh)
+        dt.render_async(scene, g, 240, out, tile, stream=sh)
         if evs is not None:
             evs[1].record(stream)
         if world > 1:
-            split.gather(slab, gathered if rank == 0 else None)
-            if rank == 0:
-                split.assemble(gathered, image)
+            pipe.submit(k)
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        step(k)
+    finish_pending()
     torch.cuda.synchronize()
     stats = dt.collect_stats(scene, sh)
 
@@ -134,7 +140,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
+        step(k, evs[k])
+    finish_pending()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -20,14 +20,46 @@ class FrameSplit:
         # equal-size slabs (rank 0 owns the most tiles) so a plain gather works
         self.slab_floats = slab_floats_max(g, self.base)
 
-    def gather(self, slab, gathered, group=None):
-        """gather the per-rank slabs into `gathered` (world*slab_floats) on rank 0."""
+    def gather(self, slab, gathered, group=None, async_op=False):
+        """gather the per-rank slabs into `gathered` (world*slab_floats) on rank 0. With
+        async_op the collective's Work is returned (wait() before reading `gathered`)."""
         import torch.distributed as dist
         if self.world == 1:
             gathered.copy_(slab)
-            return
+            return None
         parts = list(gathered.view(self.world, self.slab_floats).unbind(0)) if self.rank == 0 else None
-        dist.gather(slab, gather_list=parts, dst=0, group=group)
+        return dist.gather(slab, gather_list=parts, dst=0, group=group, async_op=async_op)
 
     def assemble(self, gathered, image):
         unpack_slabs(self.g, self.base, self.world, gathered, image)
+
+
+class GatherPipeline:
+    """Double-buffered frame gather: frame k renders into slab k%2; submit(k) starts its gather
+    (async collective) and first completes frame k-1's (wait + scatter into the image on rank
+    0), so one frame's gather runs beside the next frame's render. finish() drains."""
+
+    def __init__(self, split, slabs, gathered, image):
+        self.split = split
+        self.slabs = slabs          # two per-rank slab buffers
+        self.gathered = gathered    # two world*slab_floats buffers on rank 0 (ignored elsewhere)
+        self.image = image
+        self.pending = None
+
+    def slab(self, k):
+        return self.slabs[k % 2]
+
+    def submit(self, k):
+        self.finish()
+        b = k % 2
+        work = self.split.gather(self.slabs[b], self.gathered[b] if self.split.rank == 0 else None, async_op=True)
+        self.pending = (work, b)
+
+    def finish(self):
+        if self.pending is None:
+            return
+        work, b = self.pending
+        self.pending = None
+        work.wait()
+        if self.split.rank == 0:
+            self.split.assemble(self.gathered[b], self.image)

@@ -57,6 +57,50 @@ def _worker(rank, world, port, cfg, result_path):
         dist.destroy_process_group()
 
 
+def _pipe_worker(rank, world, port, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from distraytracer_amd.multigpu import FrameSplit, GatherPipeline
+        g, b = _scene("spheres")
+        split = FrameSplit(g, world, rank)
+        z = lambda n: torch.zeros(n, dtype=torch.float32)
+        pipe = GatherPipeline(split, [z(split.slab_floats), z(split.slab_floats)],
+                              [z(world * split.slab_floats), z(world * split.slab_floats)],
+                              z(3 * g.xRes * g.yRes))
+        images = []
+        for k in range(3):   # frame k renders with seed k, as bench.py's steps render frames
+            g.seed = k
+            slab = pipe.slab(k).numpy()
+            slab[:] = 0
+            oracle.render(b, g, 240, split.tile, out=slab, nthreads=2)
+            pipe.submit(k)   # completes frame k-1 into the image, starts frame k's gather
+            if rank == 0 and k > 0:
+                images.append(pipe.image.numpy().copy())
+        pipe.finish()
+        if rank == 0:
+            images.append(pipe.image.numpy().copy())
+            np.save(result_path, np.stack(images))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_pipeline_double_buffer(tmp_path):
+    """bench.py's pipelined gather (frame k's gather beside frame k+1's render, two slab
+    buffers): after every submit the image holds exactly the previous frame."""
+    import distraytracer_amd as dt
+    import oracle
+    out = str(tmp_path / "imgs.npy")
+    mp.start_processes(_pipe_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    got = np.load(out)
+    g, b = _scene("spheres")
+    for k in range(3):
+        g.seed = k
+        ref, _ = oracle.render(b, g, 240, dt.tiles(), nthreads=4)
+        assert np.array_equal(got[k], ref), k
+
+
 @pytest.mark.parametrize("world,cfg", [(2, "final"), (3, "spheres")])
 def test_tile_split_gather_equals_single_rank(tmp_path, world, cfg):
     import distraytracer_amd as dt
