@@ -1195,7 +1195,8 @@ __device__ __forceinline__ float schlick_complex(float cos_theta, double r0, dou
 // One full rayColor tree for the lanes with `active`. Appends to out.color in the
 // reference's accumulation order.
 __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t rootkey, float shift,
-                         PassOut& out, Entry* stack, Counters& cnt, double (*nrec)[DT_WAVE])
+                         PassOut& out, Entry* stack, Counters& cnt, double (*nrec)[DT_WAVE],
+                         double (*ocol)[DT_WAVE])
 {
   const DScene& S = *c.S;
   const DParams& P = *c.P;
@@ -1213,7 +1214,10 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     while (sp > 0) {
       e = stack[--sp];
       if (e.depth < 0) {
-        out.color = add(out.color, e.a);
+        const int l = threadIdx.x & (DT_WAVE - 1);   // out.color += own light (in LDS)
+        ocol[0][l] = ocol[0][l] + e.a.x;
+        ocol[1][l] = ocol[1][l] + e.a.y;
+        ocol[2][l] = ocol[2][l] + e.a.z;
       } else if (e.depth > 0) {
         have = true;
         break;
@@ -1551,6 +1555,29 @@ __device__ __forceinline__ void store_pixel(const DParams& P, float* out, int x,
   out[off + 2] = clampf01((float)color.z) * 255.0f;
 }
 
+// getPerspEyeRay + DoF jitter (render_final_project.cpp:195-210, 1044-1072; helpers.h:320-324):
+// the sample's eye point and the unnormalised ray through the pixel's focal point
+__device__ __forceinline__ void camera_ray(const Ctx& c, const DParams& P, int px_x, int px_y, V3& eye_sample,
+                                           V3& ray0)
+{
+  const V3 eye = v3a(P.eye), X = v3a(P.X), Y = v3a(P.Y), Z = v3a(P.Z);
+  eye_sample = eye;
+  if (P.aperture > 0) {
+    double u0, u1;
+    c.rng.draw(0, P_DOF, 0, u0, u1);
+    float r = (float)(P.aperture / 2 * u0);
+    float theta = (float)(2 * M_PI * u1);
+    double st, ct;
+    cr_sincos_d(theta, st, ct);
+    eye_sample = add(add(eye, mul(r * (float)ct, X)), mul(r * (float)st, Y));
+  }
+  float a = P.l + (P.r - P.l) * (float)px_x / (float)P.xRes;
+  float b = P.b + (P.t - P.b) * (float)px_y / (float)P.yRes;
+  V3 rayDir = sub(add(mul(a, X), mul(b, Y)), mul(P.near_plane, Z));
+  V3 focalPoint = add(eye, mul(P.focal_length, rayDir));
+  ray0 = sub(focalPoint, eye_sample);
+}
+
 struct DLaunch {
   DScene S;
   DParams P;
@@ -1564,9 +1591,15 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
 {
   const DScene& S = Lp->S;
   const DParams& P = Lp->P;
-  __shared__ double red[DT_WAVE * 3];
-  __shared__ float dens[DT_CLOUD_CHUNK];
-  __shared__ double nrec[9][DT_WAVE];   // per-lane shading record across the shadow walks
+  // LDS (one wave per block). nrec holds a lane's shading record across the shadow walks
+  // (inside run_pass only); red (per-chunk sample colours) and dens (cloud march chunk) are
+  // used after the passes, so they share its space. ocol: the DFS colour accumulator,
+  // psum: the per-pixel sums, parked here instead of in registers across the DFS.
+  __shared__ double nrec[9][DT_WAVE];
+  double* const red = &nrec[0][0];                        // DT_WAVE * 3 doubles
+  float* const dens = (float*)(&nrec[0][0] + DT_WAVE * 3);  // DT_CLOUD_CHUNK floats
+  __shared__ double ocol[3][DT_WAVE];
+  __shared__ double psum[3][DT_WAVE];
   __shared__ double chan[4];
   __shared__ unsigned long long item_s;
   Entry stack[DT_STACK_MAX];
@@ -1595,7 +1628,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     // lanes: pixel slot j = lane / min(spp,64), sample = chunk*64 + lane % ...
     const int per = spp < DT_WAVE ? spp : DT_WAVE;
     const int j = lane / per;
-    V3 pix_sum = v3(0, 0, 0);   // lane j (< group) accumulates pixel j in sample order
+    psum[0][lane] = 0; psum[1][lane] = 0; psum[2][lane] = 0;   // lane j (< group): pixel j, sample order
     int px_x = 0, px_y = 0;
     int64_t px_off = 0;
     bool px_valid = false;
@@ -1608,24 +1641,6 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       c.rng.sample = (uint32_t)sample;
 
       DT_T(k0);
-      // camera ray (cpp:1044-1072)
-      V3 eye = v3a(P.eye), X = v3a(P.X), Y = v3a(P.Y), Z = v3a(P.Z);
-      V3 eye_sample = eye;
-      if (P.aperture > 0) {
-        double u0, u1;
-        c.rng.draw(0, P_DOF, 0, u0, u1);
-        float r = (float)(P.aperture / 2 * u0);
-        float theta = (float)(2 * M_PI * u1);
-        double st, ct;
-        cr_sincos_d(theta, st, ct);
-        eye_sample = add(add(eye, mul(r * (float)ct, X)), mul(r * (float)st, Y));
-      }
-      float a = P.l + (P.r - P.l) * (float)px_x / (float)P.xRes;
-      float b = P.b + (P.t - P.b) * (float)px_y / (float)P.yRes;
-      V3 rayDir = sub(add(mul(a, X), mul(b, Y)), mul(P.near_plane, Z));
-      V3 focalPoint = add(eye, mul(P.focal_length, rayDir));
-      V3 ray0 = sub(focalPoint, eye_sample);
-
       // pass 0: the sample's rayColor tree; passes 1..blur_samples: motion-blur re-traces for
       // samples whose last hit was a moving shape (cpp:1095-1210). One call site so the DFS is
       // inlined once.
@@ -1650,11 +1665,16 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
             }
           }
         }
+        // camera ray (cpp:1044-1072), regenerated per pass from the counter RNG (same values)
+        // so that it is not held in registers across the DFS
+        V3 eye_sample = v3a(P.eye), ray0 = v3(0, 0, 0);
+        if (act) camera_ray(c, P, px_x, px_y, eye_sample, ray0);
         PassOut po;
-        po.color = v3(0, 0, 0);
+        ocol[0][lane] = 0; ocol[1][lane] = 0; ocol[2][lane] = 0;
         po.hit = pass > 0;
         po.in_motion = false;
-        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt, nrec);
+        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt, nrec, ocol);
+        po.color = v3(ocol[0][lane], ocol[1][lane], ocol[2][lane]);
         if (pass == 0) {
           tmp_color = po.color;
           hit0 = po.hit;
@@ -1675,6 +1695,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
             int64_t qo;
             bool qv;
             pixel_of(P, item * group + jj, qx, qy, qo, qv);
+            const V3 eye = v3a(P.eye), X = v3a(P.X), Y = v3a(P.Y), Z = v3a(P.Z);
             float aa = P.l + (P.r - P.l) * (float)qx / (float)P.xRes;
             float bb = P.b + (P.t - P.b) * (float)qy / (float)P.yRes;
             V3 rd = sub(add(mul(aa, X), mul(bb, Y)), mul(P.near_plane, Z));
@@ -1702,8 +1723,11 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         const int base = lane * per;
         int ns = spp - chunk * DT_WAVE;
         if (ns > per) ns = per;
-        for (int s = 0; s < ns; ++s)
-          pix_sum = add(pix_sum, v3(red[(base + s) * 3], red[(base + s) * 3 + 1], red[(base + s) * 3 + 2]));
+        {
+          V3 ps = v3(psum[0][lane], psum[1][lane], psum[2][lane]);
+          for (int s = 0; s < ns; ++s) ps = add(ps, v3(red[(base + s) * 3], red[(base + s) * 3 + 1], red[(base + s) * 3 + 2]));
+          psum[0][lane] = ps.x; psum[1][lane] = ps.y; psum[2][lane] = ps.z;
+        }
       }
       __syncthreads();
     }
@@ -1714,7 +1738,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       bool qv;
       pixel_of(P, item * group + lane, qx, qy, qo, qv);
       if (qv) {
-        V3 color = divs(pix_sum, spp);
+        V3 color = divs(v3(psum[0][lane], psum[1][lane], psum[2][lane]), spp);
         store_pixel(P, out, qx, qy, qo, color);
         if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
       }
