@@ -5,6 +5,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -29,6 +30,7 @@ thread_local std::string g_err;
 // must match the device-side DScene (dt_kernels.hip)
 struct HScene {
   const void* nodes;
+  const void* fnodes;
   const int32_t* leaf_idx;
   const void* hdr;
   const double* geom;
@@ -88,6 +90,8 @@ struct dt_scene {
   int device = 0;
   FlatScene flat;
   void* d_nodes = nullptr;
+  void* d_fnodes = nullptr;
+  int n_fnodes = 0;
   void* d_leaf = nullptr;
   void* d_hdr = nullptr;
   void* d_geom = nullptr;
@@ -198,7 +202,15 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
       o.aux = h.off;
     }
   }
-  if ((rc = upload(dnodes, &s->d_nodes)) || (rc = upload(leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
+  // Alternative traversal tree (host_fasttree.cpp): exact by construction, but on the C3 scene
+  // the reference's own SAH tree walks faster (1658 vs 1563 Mpixel-samples/s), so it is opt-in
+  // (DT_FAST_TREE=1) until a builder beats it.
+  std::vector<dtd::DNodeDev> fnodes;
+  const char* ft = getenv("DT_FAST_TREE");
+  if (!(ft && ft[0] == '1') || !build_fast_tree(dnodes, fnodes)) fnodes.clear();
+  s->n_fnodes = (int)fnodes.size();
+  if (fnodes.empty()) fnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
+  if ((rc = upload(dnodes, &s->d_nodes)) || (rc = upload(fnodes, &s->d_fnodes)) || (rc = upload(leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
       (rc = upload(f.geom, &s->d_geom)) || (rc = upload(f.mat, &s->d_mat)) || (rc = upload(f.lights, &s->d_lights)) ||
       (rc = upload(f.tex, &s->d_tex))) {
     dt_scene_destroy(s);
@@ -219,7 +231,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
 void dt_scene_destroy(dt_scene* s)
 {
   if (!s) return;
-  void* bufs[] = {s->d_nodes, s->d_leaf, s->d_hdr, s->d_geom, s->d_mat, s->d_lights, s->d_tex, s->d_zs,
+  void* bufs[] = {s->d_nodes, s->d_fnodes, s->d_leaf, s->d_hdr, s->d_geom, s->d_mat, s->d_lights, s->d_tex, s->d_zs,
                   s->d_stats, s->d_launch};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -298,6 +310,7 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   zs = cloud_z_steps(*g);
   if (g->perlin_cloud && zs.size() > 2048) return fail(DT_E_LIMIT, "clouddist/0.05 exceeds 2048 march steps");
   P.n_nodes = (int32_t)sc->flat.bvh.nodes.size();
+  P.n_fnodes = sc->n_fnodes;
 
   P.n_lights = (int32_t)sc->flat.lights.size();
   P.n_shapes = (int32_t)sc->flat.hdr.size();
@@ -322,6 +335,7 @@ static int enqueue_render(dt_scene* sc, const dtd::DParams& P, const std::vector
   if (nz) memcpy(sc->h_zs, zs.data(), nz * sizeof(float));
   HScene hs;
   hs.nodes = sc->d_nodes;
+  hs.fnodes = sc->d_fnodes;
   hs.leaf_idx = (const int32_t*)sc->d_leaf;
   hs.hdr = sc->d_hdr;
   hs.geom = (const double*)sc->d_geom;

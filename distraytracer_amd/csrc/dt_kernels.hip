@@ -82,7 +82,8 @@ __device__ __forceinline__ const DT_CAS T* cas(const T* p)
 typedef const DT_CAS double* GP;
 
 struct DScene {
-  const DNodeDev* nodes;
+  const DNodeDev* nodes;    // the reference's tree (general walks)
+  const DNodeDev* fnodes;   // same leaves, SAH inner nodes (host_fasttree.cpp; fast walks)
   const int32_t* leaf_idx;
   const DShapeHdr* hdr;
   const double* geom;
@@ -546,7 +547,7 @@ __device__ bool segment_hit(V3 A, V3 B, V3 ray, V3 origin)
 
 // GeoPrimitive::intersect. t only written when the reference writes it (Q16).
 __device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, GP g,
-                          V3 ray, V3 start, float shift, float& t, int& inside, V3& ccol, int& has_ccol)
+                          V3 ray, V3 start, float shift, float& t, int& inside, V3& ccol, int& has_ccol, int& edge)
 {
   has_ccol = 0;
   switch (type) {
@@ -599,6 +600,7 @@ __device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, GP
             segment_hit(B, C, ray, start) || segment_hit(C, D, ray, start)) {
           ccol = G3(g, CK_COL);
           has_ccol = 1;
+          edge = 1;   // t is the stale value of the previous test: order dependent
           return true;
         }
         return false;
@@ -958,6 +960,8 @@ struct Counters;
 struct HitRec {
   float t_min;
   int shape;
+  int rank;       // leaf rank of the hit in the reference's gather order (fast-tree ties)
+  int edge;       // a checkerboard edge-on hit (Q16) was taken
   int inside;
   int has_ccol;
   V3 ccol;
@@ -968,17 +972,20 @@ template <bool GENERAL, class CNT>
 __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams& P, const Walk& w, bool active, V3 ray,
                                                  V3 org, float shift, HitRec& h, CNT& cnt)
 {
+  const DNodeDev* const NODES = GENERAL ? S.nodes : S.fnodes;
   int resume = active ? 0 : 0x7fffffff;
   float t_dist = FLT_MAX;
   bool any = false;
   h.t_min = FLT_MAX;
   h.shape = -1;
+  h.rank = 0x7fffffff;
+  h.edge = 0;
   h.inside = 0;
   h.has_ccol = 0;
   int i = 0;
-  const int n_nodes = P.n_nodes;
+  const int n_nodes = GENERAL ? P.n_nodes : P.n_fnodes;
   while (i < n_nodes) {
-    const DNodeDev nd = cas(S.nodes)[i];
+    const DNodeDev nd = cas(NODES)[i];
     const bool act = resume <= i;
     const float tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
     const bool hb = act & node_hit<GENERAL>(w, nd, shift, org, tcull);
@@ -996,9 +1003,13 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
             DT_WORK(cnt.prim++);
             int ins = 0, hc = 0;
             V3 cc;
-            if (shape_hit(S, sid, type, flags, cas(S.geom) + off, ray, org, shift, t_dist, ins, cc, hc)) {
+            if (shape_hit(S, sid, type, flags, cas(S.geom) + off, ray, org, shift, t_dist, ins, cc, hc, h.edge)) {
               any = true;
-              if (t_dist < h.t_min) {
+              // strict < in the reference's gather order; the fast tree visits leaves in another
+              // order, so equal distances go to the lower reference rank
+              const int rank = GENERAL ? 0 : (int)(nd.meta >> 16);
+              if (t_dist < h.t_min || (!GENERAL && t_dist == h.t_min && rank < h.rank)) {
+                h.rank = rank;
                 h.shape = sid;
                 h.inside = ins;
                 h.t_min = t_dist;
@@ -1024,8 +1035,13 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
                                             HitRec& h, CNT& cnt)
 {
   const Walk w = make_walk(active, ray, org, shift);
-  if (w.inf_wave || w.bump_wave) return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
-  return closest_hit_walk<false>(S, P, w, active, ray, org, shift, h, cnt);
+  if (w.inf_wave || w.bump_wave || P.n_fnodes == 0)
+    return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
+  const bool any = closest_hit_walk<false>(S, P, w, active, ray, org, shift, h, cnt);
+  // an edge-on checkerboard hit keeps the previous test's t (Q16): only the reference order
+  // reproduces it, so such waves (never seen in practice) repeat the walk on the reference tree
+  if (__ballot(h.edge)) return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
+  return any;
 }
 
 // any-hit shadow test (cpp:806-855): box test with sray from isectP+sray*1e-3, shape test
@@ -1034,6 +1050,7 @@ template <bool GENERAL, class CNT>
 __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P, const Walk& w, bool active, V3 bstart,
                                               V3 sn, V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
 {
+  const DNodeDev* const NODES = GENERAL ? S.nodes : S.fnodes;   // any-hit: order free
   int resume = active ? 0 : 0x7fffffff;
   bool occl = false;
   // an occluder at distance t' < t_max along sn from sstart sits at sray-parameter
@@ -1043,9 +1060,9 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
   return false;
 #endif
   int i = 0;
-  const int n_nodes = P.n_nodes;
+  const int n_nodes = GENERAL ? P.n_nodes : P.n_fnodes;
   while (i < n_nodes) {
-    const DNodeDev nd = cas(S.nodes)[i];
+    const DNodeDev nd = cas(NODES)[i];
     const bool act = resume <= i;
     const bool hb = act & node_hit<GENERAL>(w, nd, shift, bstart, tcull);
     DT_WORK(cnt.wnodes++; cnt.box += act);
@@ -1081,7 +1098,7 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
                                          V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
 {
   const Walk w = make_walk(active, sray, bstart, shift);
-  if (w.inf_wave || w.bump_wave)
+  if (w.inf_wave || w.bump_wave || P.n_fnodes == 0)
     return occluded_walk<true>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
   return occluded_walk<false>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 }

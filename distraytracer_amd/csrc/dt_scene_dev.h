@@ -35,7 +35,8 @@ struct alignas(16) DNodeDev {
   double lb[3];
   double ub[3];
   int32_t skip;
-  uint32_t meta;   // bit0 leaf, bit1 single shape, bits 4-7 shape type, bits 8-15 shape flags
+  uint32_t meta;   // bit0 leaf, bit1 single shape, bits 4-7 shape type, bits 8-15 shape flags,
+                   // bits 16-31 (fast tree) leaf rank in the reference's gather order
   int32_t first;   // single: shape id ; multi: first entry in leaf_idx
   int32_t aux;     // single: geom offset ; multi: shape count
 };
@@ -103,6 +104,7 @@ struct DParams {
   int32_t frame_prism, frame_blur, frame_cloud;
   int32_t reflect, nogloss, perlin_cloud;
   int32_t n_nodes, n_lights, n_shapes;
+  int32_t n_fnodes;       // fast tree (host_fasttree.cpp); 0: every wave walks the reference tree
   int32_t n_cloud_steps;
   uint32_t seed;
   float aperture, focal_length, near_plane;

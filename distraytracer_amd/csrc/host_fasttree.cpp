@@ -1,0 +1,143 @@
+// host_fasttree.cpp — the traversal tree the device walks for ordinary waves.
+//
+// Why a second tree can stand in for the reference's (helpers.h:330-472): the reference gathers a
+// leaf iff its own box and every ancestor box pass BoundingVolume::intersect
+// (geometry.cpp:2657-2740). Every ancestor box contains its descendants' boxes (setBounds over all
+// of the subtree's shapes, geometry.cpp:2642-2655), and for a finite ray the slab test is monotone
+// in the bounds: a larger box gives entries <= and exits >= those of a box inside it, the rounding
+// to float included. So a leaf whose own box passes always has passing ancestors, and the gathered
+// set is exactly {leaves whose own box passes}, whatever hierarchy sits above the leaves. This
+// tree keeps the reference's leaves (same boxes, same shape lists) under new inner nodes (binned
+// SAH over the leaf boxes, each inner box the exact union of its leaves), so it gathers the same
+// leaves with fewer visits. Order only matters for the closest-hit tie rule (strict <, first in
+// the reference's gather order): every leaf carries its rank in that order and the device breaks
+// equal-t ties by rank. Not monotone, hence never used: motion-blur leaf bumps (Q19, interior
+// boxes unbumped) and axis-parallel rays (isinf branch); those waves walk the reference tree.
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "host_internal.h"
+
+namespace dth {
+
+namespace {
+
+struct LeafRef {
+  double lb[3], ub[3], c[3];
+  int node;   // index of the leaf in the reference's flattened tree
+  int rank;   // its position in the reference's gather order
+};
+
+double area(const double lb[3], const double ub[3])
+{
+  double d0 = ub[0] - lb[0], d1 = ub[1] - lb[1], d2 = ub[2] - lb[2];
+  return 2 * (d0 * d1 + d1 * d2 + d2 * d0);
+}
+
+struct Builder {
+  const std::vector<dtd::DNodeDev>& ref;   // reference tree, device format
+  std::vector<LeafRef> leaves;
+  std::vector<dtd::DNodeDev> out;
+
+  explicit Builder(const std::vector<dtd::DNodeDev>& r) : ref(r) {}
+
+  void box_of(const std::vector<int>& ids, int lo, int hi, double lb[3], double ub[3]) const
+  {
+    for (int a = 0; a < 3; ++a) { lb[a] = INFINITY; ub[a] = -INFINITY; }
+    for (int k = lo; k < hi; ++k)
+      for (int a = 0; a < 3; ++a) {
+        lb[a] = std::min(lb[a], leaves[ids[k]].lb[a]);
+        ub[a] = std::max(ub[a], leaves[ids[k]].ub[a]);
+      }
+  }
+
+  int build(std::vector<int>& ids, int lo, int hi)
+  {
+    const int me = (int)out.size();
+    out.emplace_back();
+    if (hi - lo == 1) {
+      const LeafRef& L = leaves[ids[lo]];
+      dtd::DNodeDev nd = ref[L.node];
+      nd.meta = (nd.meta & 0xffffu) | ((uint32_t)L.rank << 16);
+      nd.skip = me + 1;
+      out[me] = nd;
+      return me;
+    }
+    // SAH sweep on each axis over the leaf-box centroids
+    int best_axis = 0, best_split = lo + (hi - lo) / 2;
+    double best_cost = INFINITY;
+    std::vector<double> right_area(hi - lo + 1);
+    for (int axis = 0; axis < 3; ++axis) {
+      std::sort(ids.begin() + lo, ids.begin() + hi, [&](int a, int b) {
+        if (leaves[a].c[axis] != leaves[b].c[axis]) return leaves[a].c[axis] < leaves[b].c[axis];
+        return leaves[a].rank < leaves[b].rank;
+      });
+      double rl[3] = {INFINITY, INFINITY, INFINITY}, ru[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (int k = hi - 1; k > lo; --k) {
+        for (int a = 0; a < 3; ++a) {
+          rl[a] = std::min(rl[a], leaves[ids[k]].lb[a]);
+          ru[a] = std::max(ru[a], leaves[ids[k]].ub[a]);
+        }
+        right_area[k - lo] = area(rl, ru);
+      }
+      double ll[3] = {INFINITY, INFINITY, INFINITY}, lu[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (int k = lo; k < hi - 1; ++k) {
+        for (int a = 0; a < 3; ++a) {
+          ll[a] = std::min(ll[a], leaves[ids[k]].lb[a]);
+          lu[a] = std::max(lu[a], leaves[ids[k]].ub[a]);
+        }
+        const double cost = area(ll, lu) * (k - lo + 1) + right_area[k + 1 - lo] * (hi - k - 1);
+        if (cost < best_cost) {
+          best_cost = cost;
+          best_axis = axis;
+          best_split = k + 1;
+        }
+      }
+    }
+    std::sort(ids.begin() + lo, ids.begin() + hi, [&](int a, int b) {
+      if (leaves[a].c[best_axis] != leaves[b].c[best_axis]) return leaves[a].c[best_axis] < leaves[b].c[best_axis];
+      return leaves[a].rank < leaves[b].rank;
+    });
+    dtd::DNodeDev nd;
+    box_of(ids, lo, hi, nd.lb, nd.ub);
+    nd.meta = 0;
+    nd.first = 0;
+    nd.aux = 0;
+    out[me] = nd;
+    build(ids, lo, best_split);
+    build(ids, best_split, hi);
+    out[me].skip = (int)out.size();
+    return me;
+  }
+};
+
+}  // namespace
+
+// ref: the reference tree in device format (pre-order, last child first, skip links).
+// Returns false (and leaves `out` empty) when the tree cannot carry 16-bit leaf ranks.
+bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNodeDev>& out)
+{
+  out.clear();
+  Builder b(ref);
+  for (size_t i = 0; i < ref.size(); ++i) {
+    if (!(ref[i].meta & dtd::DN_LEAF)) continue;
+    LeafRef L;
+    for (int a = 0; a < 3; ++a) {
+      L.lb[a] = ref[i].lb[a];
+      L.ub[a] = ref[i].ub[a];
+      L.c[a] = 0.5 * (L.lb[a] + L.ub[a]);
+    }
+    L.node = (int)i;
+    L.rank = (int)b.leaves.size();
+    b.leaves.push_back(L);
+  }
+  if (b.leaves.empty() || b.leaves.size() > 0xffff) return false;
+  std::vector<int> ids(b.leaves.size());
+  for (size_t i = 0; i < ids.size(); ++i) ids[i] = (int)i;
+  b.build(ids, 0, (int)ids.size());
+  out.swap(b.out);
+  return true;
+}
+
+}  // namespace dth

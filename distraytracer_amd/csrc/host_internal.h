@@ -18,6 +18,8 @@ struct FlatBVH {
 
 void shape_bounds(const dt_shape_desc& sh, dtm::V3& lb, dtm::V3& ub);
 void build_bvh(const dt_scene_desc& d, const dt_globals& g, FlatBVH& out);
+// host_fasttree.cpp: same leaves, SAH inner nodes, 16-bit leaf ranks in meta (false: no fast tree)
+bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNodeDev>& out);
 
 // device-layout scene produced from a descriptor (host_flatten.cpp)
 struct FlatScene {
