@@ -896,7 +896,8 @@ __device__ __forceinline__ bool box_hit_exact_finite(const DNodeDev& b, const Ra
 // light). A shape lies inside its leaf box (bounds of its own vertices/extent, +-1e-2 leaf
 // padding), so a culled box holds no hit the reference would have used: the result is
 // unchanged, only the gather is smaller. Callers pass FLT_MAX to disable it.
-// (An f32 pre-test with an exact fallback was measured slower: 1515 vs 1606 Msps on C3.)
+// (Measured slower and dropped: an f32 pre-test with an exact fallback, 1515 vs 1606 Msps on C3;
+// wave-uniform slab-end selection for sign-coherent waves, 1482 vs 1630.)
 __device__ __forceinline__ bool box_hit_finite(const DNodeDev& b, const RayBox& r, V3 st, float tcull)
 {
   return box_hit_exact_finite(b, r, st, tcull);
@@ -972,7 +973,9 @@ template <bool GENERAL, class CNT>
 __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams& P, const Walk& w, bool active, V3 ray,
                                                  V3 org, float shift, HitRec& h, CNT& cnt)
 {
-  const DNodeDev* const NODES = GENERAL ? S.nodes : S.fnodes;
+  // fast walks use the alternative tree when one was built (DT_FAST_TREE), else the reference's
+  const bool ftree = !GENERAL && P.n_fnodes > 0;
+  const DNodeDev* const NODES = ftree ? S.fnodes : S.nodes;
   int resume = active ? 0 : 0x7fffffff;
   float t_dist = FLT_MAX;
   bool any = false;
@@ -983,7 +986,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
   h.inside = 0;
   h.has_ccol = 0;
   int i = 0;
-  const int n_nodes = GENERAL ? P.n_nodes : P.n_fnodes;
+  const int n_nodes = ftree ? P.n_fnodes : P.n_nodes;
   while (i < n_nodes) {
     const DNodeDev nd = cas(NODES)[i];
     const bool act = resume <= i;
@@ -1007,8 +1010,8 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
               any = true;
               // strict < in the reference's gather order; the fast tree visits leaves in another
               // order, so equal distances go to the lower reference rank
-              const int rank = GENERAL ? 0 : (int)(nd.meta >> 16);
-              if (t_dist < h.t_min || (!GENERAL && t_dist == h.t_min && rank < h.rank)) {
+              const int rank = ftree ? (int)(nd.meta >> 16) : 0;
+              if (t_dist < h.t_min || (ftree && t_dist == h.t_min && rank < h.rank)) {
                 h.rank = rank;
                 h.shape = sid;
                 h.inside = ins;
@@ -1035,12 +1038,12 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
                                             HitRec& h, CNT& cnt)
 {
   const Walk w = make_walk(active, ray, org, shift);
-  if (w.inf_wave || w.bump_wave || P.n_fnodes == 0)
-    return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
+  if (w.inf_wave || w.bump_wave) return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
   const bool any = closest_hit_walk<false>(S, P, w, active, ray, org, shift, h, cnt);
   // an edge-on checkerboard hit keeps the previous test's t (Q16): only the reference order
-  // reproduces it, so such waves (never seen in practice) repeat the walk on the reference tree
-  if (__ballot(h.edge)) return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
+  // reproduces it, so with the alternative tree such waves (never seen in practice) repeat the
+  // walk on the reference tree
+  if (P.n_fnodes > 0 && __ballot(h.edge)) return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
   return any;
 }
 
@@ -1050,7 +1053,9 @@ template <bool GENERAL, class CNT>
 __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P, const Walk& w, bool active, V3 bstart,
                                               V3 sn, V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
 {
-  const DNodeDev* const NODES = GENERAL ? S.nodes : S.fnodes;   // any-hit: order free
+  // fast walks use the alternative tree when one was built (DT_FAST_TREE), else the reference's
+  const bool ftree = !GENERAL && P.n_fnodes > 0;
+  const DNodeDev* const NODES = ftree ? S.fnodes : S.nodes;   // any-hit: order free
   int resume = active ? 0 : 0x7fffffff;
   bool occl = false;
   // an occluder at distance t' < t_max along sn from sstart sits at sray-parameter
@@ -1060,7 +1065,7 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
   return false;
 #endif
   int i = 0;
-  const int n_nodes = GENERAL ? P.n_nodes : P.n_fnodes;
+  const int n_nodes = ftree ? P.n_fnodes : P.n_nodes;
   while (i < n_nodes) {
     const DNodeDev nd = cas(NODES)[i];
     const bool act = resume <= i;
@@ -1098,7 +1103,7 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
                                          V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
 {
   const Walk w = make_walk(active, sray, bstart, shift);
-  if (w.inf_wave || w.bump_wave || P.n_fnodes == 0)
+  if (w.inf_wave || w.bump_wave)
     return occluded_walk<true>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
   return occluded_walk<false>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 }
