@@ -193,7 +193,12 @@ def main():
                          "traffic_source": ("profiles/%s_summary.json (2*FETCH_SIZE + WRITE_SIZE, fabric requests "
                                             "incl. Infinity-Cache hits: an upper bound on HBM bytes)" % pmc.get("tag"))
                          if traffic else None,
-                         "valu_active_per_wave_cycle": pmc.get("valu_active_per_wave_cycle"),
+                         "valu": ({"active_per_wave_cycle": pmc.get("valu_active_per_wave_cycle"),
+                                   "simd_busy": round(4 * pmc["valu_active_per_wave_cycle"], 3),
+                                   "lane_utilisation": pmc.get("valu_lane_utilisation"),
+                                   "note": "binding unit (SURVEY 8d): VALU issue, 4 waves/SIMD; from the "
+                                           "committed PMC profile of this kernel"}
+                                  if pmc.get("valu_active_per_wave_cycle") else None),
                          "kernel": "dt_trace_kernel", "kernel_ms": round(kernel_ms, 3),
                          "alg_bytes_per_launch": int(alg_bytes),
                          "note": "VALU-bound path (FP64 intersection/shading); HBM fraction reported as "

@@ -57,7 +57,8 @@ def main(tag, kernel="dt_trace_kernel"):
     # the profile bench.py's roofline.traffic reads (the latest summarised tag)
     with open(os.path.join(ROOT, "profiles", "pmc_trace_summary.json"), "w") as fh:
         json.dump({k: out.get(k) for k in ("tag", "kernel", "avg_duration_ns", "hbm_bytes_per_launch",
-                                            "valu_active_per_wave_cycle", "valu_lane_utilisation")},
+                                            "valu_active_per_wave_cycle", "valu_lane_utilisation",
+                                            "fp64_tflops_upper")},
                   fh, indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
     return out
