@@ -51,11 +51,33 @@ def cpu_baseline(dt, cfg, frac_world):
     t0 = time.perf_counter()
     _, st = oracle.render(built, g, 240, tile, out=out, nthreads=threads)
     dt_s = time.perf_counter() - t0
+    # single-core figure on a smaller slice (SURVEY 8d asks for both)
+    tile1 = dt.tiles(rank=0, world=frac_world * 16, layout=dt.DT_OUT_SLAB)
+    out1 = np.zeros(dt.slab_floats(g, tile1), dtype=np.float32)
+    t1 = time.perf_counter()
+    _, st1 = oracle.render(built, g, 240, tile1, out=out1, nthreads=1)
+    dt1 = time.perf_counter() - t1
     return {"value": round(st.samples / dt_s / 1e6, 4), "unit": "Mpixel-samples/s", "cores": threads,
             "kind": "port",
             "sample": "oracle/oracle.c (OpenMP) on 1/%d of the frame's 32x32 tiles (rank-0 of a %d-way "
                       "interleave: %d pixels x %d spp), %.1f s wall" % (frac_world, frac_world, st.pixels,
-                                                                    st.samples // max(st.pixels, 1), dt_s)}
+                                                                    st.samples // max(st.pixels, 1), dt_s),
+            "single_core": {"value": round(st1.samples / dt1 / 1e6, 4), "cores": 1,
+                            "sample": "1/%d of the tiles, %.1f s" % (frac_world * 16, dt1)}}
+
+
+def end_to_end_ms(dt, cfg, dev):
+    """One frame end to end as a caller of the ABI sees it: host scene build
+    (buildFinal + BVH + flatten), upload, render, D2H of the ppmOut image; file write excluded."""
+    import torch
+    t0 = time.perf_counter()
+    g, built = build_globals(dt, cfg)
+    scene = dt.Scene(built, g)
+    out = torch.empty(3 * g.xRes * g.yRes, dtype=torch.float32, pin_memory=True)
+    dt.render(scene, g, 240, out.numpy())
+    t1 = time.perf_counter()
+    scene.close()
+    return round((t1 - t0) * 1e3, 3)
 
 
 def load_pmc_traffic():
@@ -166,6 +188,7 @@ def main():
         pmc = load_pmc_traffic() or {}
         traffic = pmc.get("hbm_bytes_per_launch")
         cpu = None
+        e2e = end_to_end_ms(dt, args.config, dev) if world == 1 else None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(dt, args.config, args.cpu_frac)
         line = {
@@ -204,6 +227,7 @@ def main():
                          "note": "VALU-bound path (FP64 intersection/shading); HBM fraction reported as "
                                  "north_star asks"},
             "cpu_baseline": cpu,
+            "end_to_end_ms_per_frame": e2e,
             "work": {"rays_per_sample": round(lib_stats.rays / max(lib_stats.samples, 1), 3),
                      "shadow_rays_per_sample": round(lib_stats.shadow_rays / max(lib_stats.samples, 1), 3),
                      "stack_overflows": lib_stats.stack_overflows, "nan_pixels": lib_stats.nan_pixels},

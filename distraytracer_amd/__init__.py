@@ -159,6 +159,12 @@ def write_ppm(filename, g, values):
     check(lib.dt_write_ppm(filename.encode(), g.xRes, g.yRes, ctypes.c_void_p(v.ctypes.data)), "dt_write_ppm")
 
 
+def write_png(filename, g, values):
+    import numpy as np
+    v = np.ascontiguousarray(values, dtype=np.float32)
+    check(lib.dt_write_png(filename.encode(), g.xRes, g.yRes, ctypes.c_void_p(v.ctypes.data)), "dt_write_png")
+
+
 def renderImage(filename, frame, sceneBuilder, g=None, builder_frame=None):
     """render_final_project.cpp:965: build (sceneBuilder names a scene.h builder), render the
     frame on the current GPU, write the PPM. Returns (image, stats)."""
@@ -169,7 +175,7 @@ def renderImage(filename, frame, sceneBuilder, g=None, builder_frame=None):
     img = np.zeros(3 * g.xRes * g.yRes, dtype=np.float32)
     st = render(scene, g, frame, img)
     if filename:
-        write_ppm(filename, g, img)
+        (write_png if filename.endswith(".png") else write_ppm)(filename, g, img)
     scene.close()
     return img, st
 

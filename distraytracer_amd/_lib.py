@@ -99,7 +99,7 @@ class BVHNode(ctypes.Structure):
 EXPORTS = ["dt_abi_version", "dt_last_error", "dt_globals_default", "dt_scene_create", "dt_scene_destroy",
            "dt_scene_bvh", "dt_bvh_build", "dt_slab_floats", "dt_slab_floats_max", "dt_render", "dt_render_async",
            "dt_collect_stats", "dt_debug_counters", "dt_render_sky", "dt_unpack_slabs", "dt_build_scene", "dt_scene_desc_free",
-           "dt_write_ppm", "dt_mocap_bone_table"]
+           "dt_write_ppm", "dt_write_png", "dt_mocap_bone_table"]
 
 
 class DTError(RuntimeError):
@@ -150,6 +150,7 @@ def _load():
         "dt_build_scene": (c_int32, [ctypes.c_char_p, c_float, P(Globals), ctypes.c_char_p, P(P(SceneDesc))]),
         "dt_scene_desc_free": (None, [P(SceneDesc)]),
         "dt_write_ppm": (c_int32, [ctypes.c_char_p, c_int32, c_int32, ctypes.c_void_p]),
+        "dt_write_png": (c_int32, [ctypes.c_char_p, c_int32, c_int32, ctypes.c_void_p]),
         "dt_mocap_bone_table": (c_int32, [ctypes.c_char_p, ctypes.c_char_p, P(c_int32), c_int32,
                                           P(c_double), P(c_int32), P(c_int32)]),
     }

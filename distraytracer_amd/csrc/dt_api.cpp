@@ -2,6 +2,7 @@
 // No exception and no exit() crosses the boundary: every entry point returns a status
 // code and leaves a message for dt_last_error().
 #include <hip/hip_runtime.h>
+#include <zlib.h>
 
 #include <cmath>
 #include <cstdio>
@@ -567,6 +568,48 @@ int dt_write_ppm(const char* filename, int32_t xRes, int32_t yRes, const float* 
   if (!fp) return fail(DT_E_IO, std::string("could not open ") + filename);
   fprintf(fp, "P6\n%d %d\n255\n", xRes, yRes);
   fwrite(px.data(), 1, total, fp);
+  fclose(fp);
+  return DT_OK;
+}
+
+static void put_be32(std::vector<unsigned char>& v, uint32_t x)
+{
+  v.push_back((unsigned char)(x >> 24)); v.push_back((unsigned char)(x >> 16));
+  v.push_back((unsigned char)(x >> 8)); v.push_back((unsigned char)x);
+}
+
+int dt_write_png(const char* filename, int32_t xRes, int32_t yRes, const float* values)
+{
+  // the same 8-bit pixels as dt_write_ppm (float -> unsigned char truncation), as an RGB PNG
+  if (!filename || !values || xRes <= 0 || yRes <= 0) return fail(DT_E_INVALID, "bad arguments");
+  const size_t row = (size_t)xRes * 3;
+  std::vector<unsigned char> raw((row + 1) * (size_t)yRes);
+  for (int y = 0; y < yRes; ++y) {
+    raw[y * (row + 1)] = 0;   // filter type none
+    for (size_t i = 0; i < row; ++i) raw[y * (row + 1) + 1 + i] = (unsigned char)values[(size_t)y * row + i];
+  }
+  uLongf zlen = compressBound((uLong)raw.size());
+  std::vector<unsigned char> z(zlen);
+  if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), 6) != Z_OK) return fail(DT_E_IO, "zlib failed");
+  z.resize(zlen);
+  std::vector<unsigned char> png = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+  auto chunk = [&](const char* type, const std::vector<unsigned char>& data) {
+    put_be32(png, (uint32_t)data.size());
+    const size_t at = png.size();
+    png.insert(png.end(), type, type + 4);
+    png.insert(png.end(), data.begin(), data.end());
+    put_be32(png, (uint32_t)crc32(0L, png.data() + at, (uInt)(png.size() - at)));
+  };
+  std::vector<unsigned char> ihdr;
+  put_be32(ihdr, (uint32_t)xRes);
+  put_be32(ihdr, (uint32_t)yRes);
+  ihdr.insert(ihdr.end(), {8, 2, 0, 0, 0});   // 8-bit, RGB, deflate, no filter, no interlace
+  chunk("IHDR", ihdr);
+  chunk("IDAT", z);
+  chunk("IEND", {});
+  FILE* fp = fopen(filename, "wb");
+  if (!fp) return fail(DT_E_IO, std::string("could not open ") + filename);
+  fwrite(png.data(), 1, png.size(), fp);
   fclose(fp);
   return DT_OK;
 }

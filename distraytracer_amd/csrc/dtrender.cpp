@@ -9,7 +9,7 @@
 //   dtrender nodistr <n>     antialias 6 (1457-1469)
 //   dtrender perlin <i>      renderImageCloud 640x480 (1685-1698)
 //   dtrender spheres         buildSceneSpheres(0) 256x256 (config C1)
-// options (after the mode): --out FILE  --spp N  --depth N  --res WxH  --seed S
+// options (after the mode): --out FILE(.ppm|.png)  --spp N  --depth N  --res WxH  --seed S
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -98,8 +98,9 @@ int main(int argc, char** argv)
   rc = dt_render(s, &g, frame, nullptr, img.data(), 0, nullptr, &st);
   if (rc) return die("dt_render", rc);
   std::string fn = out.empty() ? std::string(buf) : out;
-  rc = dt_write_ppm(fn.c_str(), g.xRes, g.yRes, img.data());
-  if (rc) return die("dt_write_ppm", rc);
+  const bool png = fn.size() > 4 && fn.compare(fn.size() - 4, 4, ".png") == 0;
+  rc = png ? dt_write_png(fn.c_str(), g.xRes, g.yRes, img.data()) : dt_write_ppm(fn.c_str(), g.xRes, g.yRes, img.data());
+  if (rc) return die("dt_write_ppm/png", rc);
   double msps = st.samples / (st.kernel_ms * 1e-3) / 1e6;
   printf("Rendered %s frame %d: %dx%d, %d spp, depth %d in %.2f ms (kernel, %.1f Mpixel-samples/s) -> %s\n",
          scene.c_str(), frame, g.xRes, g.yRes, (int)st.samples / (g.xRes * g.yRes), g.max_depth, st.kernel_ms,

@@ -215,9 +215,9 @@ typedef struct dt_stats {
   uint64_t nan_pixels;
   uint64_t tex_fetches;       /* texel reads (algorithmic bytes) */
   uint64_t stack_overflows;   /* DFS entries dropped (device stack limit); 0 when validated */
-  uint64_t box_tests;         /* lane-level BVH slab tests (work counter, DESIGN.md roofline) */
-  uint64_t prim_tests;        /* lane-level primitive intersect/intersectShadow calls */
-  uint64_t wave_node_visits;  /* wave-level BVH node visits (union traversal) */
+  uint64_t box_tests;         /* lane-level BVH slab tests      (these three: diagnostic builds */
+  uint64_t prim_tests;        /* lane-level primitive tests       with -DDT_WORK_COUNTERS only; */
+  uint64_t wave_node_visits;  /* wave-level BVH node visits        0 otherwise)  */
   double   kernel_ms;         /* device time of the render kernels (hipEvents, same stream) */
   double   trace_kernel_ms;   /* device time of the dominant (trace) kernel alone */
 } dt_stats;
@@ -296,6 +296,8 @@ int dt_mocap_bone_table(const char* asf, const char* amc, const int32_t* frames,
 
 /* writePPM (helpers.h:174-195): float -> unsigned char truncation */
 int dt_write_ppm(const char* filename, int32_t xRes, int32_t yRes, const float* values);
+/* the same pixels as an 8-bit RGB PNG (the output surface beside PPM) */
+int dt_write_png(const char* filename, int32_t xRes, int32_t yRes, const float* values);
 
 #ifdef __cplusplus
 }

@@ -103,3 +103,25 @@ def test_write_ppm_truncates(tmp_path):
     data = p.read_bytes()
     assert data.startswith(b"P6\n2 1\n255\n")
     assert list(data[-6:]) == [0, 254, 255, 1, 100, 7]
+
+
+def test_write_png_matches_ppm_pixels(tmp_path):
+    """dt_write_png: an RGB PNG holding exactly writePPM's truncated bytes."""
+    import struct
+    import zlib
+    import numpy as np
+    g = dt.globals_default()
+    g.xRes, g.yRes = 3, 2
+    vals = np.array([0.0, 254.9, 255.0, 1.5, 100.99, 7.0, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0, 128.7, 64.2],
+                    dtype=np.float32)
+    p = tmp_path / "x.png"
+    dt.write_png(str(p), g, vals)
+    data = p.read_bytes()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    w, h, depth, ctype = struct.unpack(">IIBB", data[16:26])
+    assert (w, h, depth, ctype) == (3, 2, 8, 2)
+    i = data.index(b"IDAT")
+    n = struct.unpack(">I", data[i - 4:i])[0]
+    raw = zlib.decompress(data[i + 4:i + 4 + n])
+    rows = [raw[r * 10 + 1:(r + 1) * 10] for r in range(2)]
+    assert list(b"".join(rows)) == [int(v) for v in vals]
