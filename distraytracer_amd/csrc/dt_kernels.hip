@@ -1083,7 +1083,9 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
           const bool test = hb && !occl && sid != skip_shape;
           if (test) {
             DT_WORK(cnt.prim++);
+#ifndef DT_ABL_NOPRIM_SHADOW
             if (shape_shadow(type, flags, cas(S.geom) + off, sn, sstart, t_max, shift)) occl = true;
+#endif
           }
         }
       }
@@ -1105,6 +1107,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   const Walk w = make_walk(active, sray, bstart, shift);
   if (w.inf_wave || w.bump_wave)
     return occluded_walk<true>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+#ifdef DT_ABL_NOSHADOW
+  return false;
+#endif
   return occluded_walk<false>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 }
 
@@ -1482,6 +1487,11 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           }
           V3 ray_col;
           const float roughness = M.roughness;
+#ifdef DT_ABL_NOBRDF
+          if (true) {
+            ray_col = cwise(shape_color, lc);
+          } else
+#endif
           if (M.model == DT_MODEL_OREN_NAYAR) {
             float A = (float)(1.0 - (0.5 * pw2((double)roughness)) / (pw2((double)roughness) + 0.33));
             float B = (float)((0.45 * pw2((double)roughness)) / (pw2((double)roughness) + 0.09));
