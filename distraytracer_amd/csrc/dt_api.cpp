@@ -618,7 +618,7 @@ int dt_write_png(const char* filename, int32_t xRes, int32_t yRes, const float* 
 
 extern "C" int dt_debug_counters(const dt_scene* sc, uint64_t* out, int32_t n)
 {
-  if (!sc || !out || n < 0 || n > 32) return fail(DT_E_INVALID, "bad arguments");
+  if (!sc || !out || n < 0 || n > 39) return fail(DT_E_INVALID, "bad arguments");
   unsigned long long h[ST_N + 40];
   HIPCHK(hipMemcpy(h, sc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
   for (int i = 0; i < n; ++i) out[i] = h[ST_N + 1 + i];

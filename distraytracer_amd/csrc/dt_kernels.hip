@@ -993,8 +993,10 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
     const float tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
     const bool hb = act & node_hit<GENERAL>(w, nd, shift, org, tcull);
     DT_WORK(cnt.wnodes++; cnt.box += act);
+    DT_CNT(26);
     if (nd.meta & DN_LEAF) {
       if (__ballot(hb)) {
+        DT_T(q0);
         const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
         for (int q = 0; q < nq; ++q) {
           int sid, type, off;
@@ -1021,6 +1023,8 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
               }
             }
           }
+        DT_T(q1);
+        DT_ACC(33, q0, q1);
         }
       }
       if (act) resume = nd.skip;
@@ -1065,14 +1069,22 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
   return false;
 #endif
   int i = 0;
+#ifdef DT_STAMPS
+  unsigned long long nv = 0;
+#endif
   const int n_nodes = ftree ? P.n_fnodes : P.n_nodes;
   while (i < n_nodes) {
     const DNodeDev nd = cas(NODES)[i];
     const bool act = resume <= i;
     const bool hb = act & node_hit<GENERAL>(w, nd, shift, bstart, tcull);
     DT_WORK(cnt.wnodes++; cnt.box += act);
+    DT_CNT(27);
+#ifdef DT_STAMPS
+    ++nv;
+#endif
     if (nd.meta & DN_LEAF) {
       if (__ballot(hb)) {
+        DT_T(q0);
         const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
         for (int q = 0; q < nq; ++q) {
           int sid, type, off;
@@ -1088,6 +1100,8 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
 #endif
           }
         }
+        DT_T(q1);
+        DT_ACC(32, q0, q1);
       }
       if (act) resume = occl ? 0x7fffffff : nd.skip;
       i = i + 1;
@@ -1097,6 +1111,13 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
     }
     if (!__ballot(resume != 0x7fffffff)) break;
   }
+#ifdef DT_STAMPS
+  {   // walks whose active lanes all ended occluded (28 visits, 29 walks) / none occluded (30, 31)
+    const unsigned long long va = __ballot(active), vo = __ballot(occl);
+    if (va && vo == va) { cnt.ph[28] += nv; cnt.ph[29] += 1; }
+    if (va && vo == 0) { cnt.ph[30] += nv; cnt.ph[31] += 1; }
+  }
+#endif
   return occl;
 }
 
@@ -1138,7 +1159,7 @@ struct Counters {
   uint32_t box, prim;
   uint32_t wnodes;                   // wave-level
 #ifdef DT_STAMPS
-  unsigned long long ph[28];   // diagnostic build only: cycles per phase, event counts (wave-uniform)
+  unsigned long long ph[40];   // diagnostic build only: cycles per phase, event counts (wave-uniform)
 #endif
 };
 
@@ -1645,7 +1666,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   Counters cnt;
   cnt.rays = 0; cnt.shadow = 0; cnt.tex = 0; cnt.box = 0; cnt.prim = 0; cnt.wnodes = 0;
 #ifdef DT_STAMPS
-  for (int k = 0; k < 28; ++k) cnt.ph[k] = 0;
+  for (int k = 0; k < 40; ++k) cnt.ph[k] = 0;
 #endif
 
   while (true) {
@@ -1784,7 +1805,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       atomicAdd(S.stats + ST_PRIM, pr);
       atomicAdd(S.stats + ST_WNODES, (unsigned long long)cnt.wnodes);
 #ifdef DT_STAMPS
-      for (int k = 0; k < 28; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);
+      for (int k = 0; k < 39; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);
 #endif
       if (sky_px) atomicAdd(S.stats + ST_SKY, sky_px);
       atomicAdd(S.stats + ST_RAYS, r);

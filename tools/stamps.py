@@ -20,8 +20,8 @@ def main():
     s = dt.Scene(b, g)
     out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
     st = dt.render(s, g, 240, out)
-    arr = (ctypes.c_uint64 * 28)()
-    dt.check(dt.lib.dt_debug_counters(s.handle, arr, 28))
+    arr = (ctypes.c_uint64 * 39)()
+    dt.check(dt.lib.dt_debug_counters(s.handle, arr, 39))
     tot = arr[5] + arr[6]
     print("kernel ms %.2f" % st.kernel_ms)
     for i, n in enumerate(NAMES[:7]):
@@ -33,6 +33,11 @@ def main():
              0: "checkercyl"}
     print("closest-hit prim tests per item:", {names[t]: round(arr[10 + t] / items, 2) for t in range(8) if arr[10 + t]})
     print("shadow prim tests per item:", {names[t]: round(arr[18 + t] / items, 2) for t in range(8) if arr[18 + t]})
+    print("node visits per item: closest-hit %.1f  shadow %.1f" % (arr[26] / items, arr[27] / items))
+    print("cycles in shadow leaf/prim blocks %.2f%%, closest-hit leaf/prim blocks %.2f%%"
+          % (100.0 * arr[32] / max(tot, 1), 100.0 * arr[33] / max(tot, 1)))
+    print("shadow walks per item: all occluded %.2f (%.1f visits/walk), none occluded %.2f (%.1f/walk), total %.2f"
+          % (arr[29] / items, arr[28] / max(arr[29], 1), arr[31] / items, arr[30] / max(arr[31], 1), arr[9] / items))
 
 
 if __name__ == "__main__":
