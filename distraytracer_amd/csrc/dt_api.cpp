@@ -93,6 +93,7 @@ struct dt_scene {
   void* d_nodes = nullptr;
   void* d_fnodes = nullptr;
   int n_fnodes = 0;
+  int ftree_mode = 0;
   void* d_leaf = nullptr;
   void* d_hdr = nullptr;
   void* d_geom = nullptr;
@@ -203,12 +204,14 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
       o.aux = h.off;
     }
   }
-  // Alternative traversal tree (host_fasttree.cpp): exact by construction, but on the C3 scene
-  // the reference's own SAH tree walks faster (1658 vs 1563 Mpixel-samples/s), so it is opt-in
-  // (DT_FAST_TREE=1) until a builder beats it.
+  // Alternative traversal tree (host_fasttree.cpp): exact by construction. Closest-hit walks use
+  // it by default; for shadow walks the reference's own SAH tree is faster on C3.
   std::vector<dtd::DNodeDev> fnodes;
+  // DT_FAST_TREE: c (default) closest-hit walks, 1 every fast walk, s shadow walks only, 0 none.
+  // On C3 closest hit walks it faster (1666 vs 1624 Mpixel-samples/s), shadow walks slower.
   const char* ft = getenv("DT_FAST_TREE");
-  if (!(ft && ft[0] == '1') || !build_fast_tree(dnodes, fnodes)) fnodes.clear();
+  s->ftree_mode = !ft ? 1 : ft[0] == '1' ? 3 : ft[0] == 'c' ? 1 : ft[0] == 's' ? 2 : 0;
+  if (!s->ftree_mode || !build_fast_tree(dnodes, fnodes)) fnodes.clear();
   s->n_fnodes = (int)fnodes.size();
   if (fnodes.empty()) fnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
   if ((rc = upload(dnodes, &s->d_nodes)) || (rc = upload(fnodes, &s->d_fnodes)) || (rc = upload(leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
@@ -312,6 +315,7 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   if (g->perlin_cloud && zs.size() > 2048) return fail(DT_E_LIMIT, "clouddist/0.05 exceeds 2048 march steps");
   P.n_nodes = (int32_t)sc->flat.bvh.nodes.size();
   P.n_fnodes = sc->n_fnodes;
+  P.ftree_mode = sc->ftree_mode;
 
   P.n_lights = (int32_t)sc->flat.lights.size();
   P.n_shapes = (int32_t)sc->flat.hdr.size();

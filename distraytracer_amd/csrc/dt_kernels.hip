@@ -974,7 +974,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
                                                  V3 org, float shift, HitRec& h, CNT& cnt)
 {
   // fast walks use the alternative tree when one was built (DT_FAST_TREE), else the reference's
-  const bool ftree = !GENERAL && P.n_fnodes > 0;
+  const bool ftree = !GENERAL && P.n_fnodes > 0 && (P.ftree_mode & 1);
   const DNodeDev* const NODES = ftree ? S.fnodes : S.nodes;
   int resume = active ? 0 : 0x7fffffff;
   float t_dist = FLT_MAX;
@@ -1047,7 +1047,7 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
   // an edge-on checkerboard hit keeps the previous test's t (Q16): only the reference order
   // reproduces it, so with the alternative tree such waves (never seen in practice) repeat the
   // walk on the reference tree
-  if (P.n_fnodes > 0 && __ballot(h.edge)) return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
+  if (P.n_fnodes > 0 && (P.ftree_mode & 1) && __ballot(h.edge)) return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
   return any;
 }
 
@@ -1058,7 +1058,7 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
                                               V3 sn, V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
 {
   // fast walks use the alternative tree when one was built (DT_FAST_TREE), else the reference's
-  const bool ftree = !GENERAL && P.n_fnodes > 0;
+  const bool ftree = !GENERAL && P.n_fnodes > 0 && (P.ftree_mode & 2);
   const DNodeDev* const NODES = ftree ? S.fnodes : S.nodes;   // any-hit: order free
   int resume = active ? 0 : 0x7fffffff;
   bool occl = false;

@@ -105,6 +105,7 @@ struct DParams {
   int32_t reflect, nogloss, perlin_cloud;
   int32_t n_nodes, n_lights, n_shapes;
   int32_t n_fnodes;       // fast tree (host_fasttree.cpp); 0: every wave walks the reference tree
+  int32_t ftree_mode;     // walks that use it: bit 0 closest hit, bit 1 shadow
   int32_t n_cloud_steps;
   uint32_t seed;
   float aperture, focal_length, near_plane;

@@ -196,18 +196,21 @@ def test_slab_layout_matches_image(cuda):
 
 
 def test_fast_tree_gathers_the_reference_leaves(cuda, monkeypatch):
-    """DT_FAST_TREE=1: the alternative traversal tree (host_fasttree.cpp, same leaves under SAH
-    inner nodes) must give the reference-tree image bit for bit (monotone slab test + rank
-    tie-break); C2 window with glossy floor, doors and area-light shadows."""
+    """The alternative traversal tree (host_fasttree.cpp, same leaves under SAH inner nodes) must
+    give the reference-tree image bit for bit (monotone slab test + rank tie-break), whichever
+    walks use it: DT_FAST_TREE=0 (none), c (closest hit, the default), s (shadow), 1 (both).
+    C2 window with glossy floor, doors and area-light shadows."""
     g = dt.globals_default()
     g.use_model = 0
     built = dt.build_scene("final", 240, g)
     g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.brdf_samples = 800, 600, 16, 4, 2
     tile = dt.tiles(x0=380, y0=250, x1=420, y1=280)
+    monkeypatch.setenv("DT_FAST_TREE", "0")
     ref_img, _ = _render_gpu(built, g, 240, tile)
-    monkeypatch.setenv("DT_FAST_TREE", "1")
-    fast_img, _ = _render_gpu(built, g, 240, tile)
-    assert np.array_equal(fast_img, ref_img)
+    for mode in ("c", "s", "1"):
+        monkeypatch.setenv("DT_FAST_TREE", mode)
+        fast_img, _ = _render_gpu(built, g, 240, tile)
+        assert np.array_equal(fast_img, ref_img), mode
 
 
 def _feature_scene():
