@@ -989,7 +989,10 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
   const int n_nodes = ftree ? P.n_fnodes : P.n_nodes;
   while (i < n_nodes) {
     const DNodeDev nd = cas(NODES)[i];
-    const bool act = resume <= i;
+    // fast walks need no per-lane resume point: every box contains its subtree's boxes and the
+    // finite-ray slab test (with the shrinking tcull) is monotone in the box, so a lane that
+    // failed an ancestor fails here too (host_fasttree.cpp)
+    const bool act = GENERAL ? resume <= i : active;
     const float tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
     const bool hb = act & node_hit<GENERAL>(w, nd, shift, org, tcull);
     DT_WORK(cnt.wnodes++; cnt.box += act);
@@ -1023,14 +1026,14 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
               }
             }
           }
+        }
         DT_T(q1);
         DT_ACC(33, q0, q1);
-        }
       }
-      if (act) resume = nd.skip;
+      if (GENERAL && act) resume = nd.skip;
       i = i + 1;
     } else {
-      if (act && !hb) resume = nd.skip;
+      if (GENERAL && act && !hb) resume = nd.skip;
       i = __ballot(hb) ? i + 1 : nd.skip;
     }
   }
@@ -1075,7 +1078,7 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
   const int n_nodes = ftree ? P.n_fnodes : P.n_nodes;
   while (i < n_nodes) {
     const DNodeDev nd = cas(NODES)[i];
-    const bool act = resume <= i;
+    const bool act = GENERAL ? resume <= i : active & !occl;   // see closest_hit_walk
     const bool hb = act & node_hit<GENERAL>(w, nd, shift, bstart, tcull);
     DT_WORK(cnt.wnodes++; cnt.box += act);
     DT_CNT(27);
@@ -1103,13 +1106,17 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
         DT_T(q1);
         DT_ACC(32, q0, q1);
       }
-      if (act) resume = occl ? 0x7fffffff : nd.skip;
+      if (GENERAL) {
+        if (act) resume = occl ? 0x7fffffff : nd.skip;
+        if (!__ballot(resume != 0x7fffffff)) break;
+      } else if (!__ballot(active & !occl)) {
+        break;
+      }
       i = i + 1;
     } else {
-      if (act && !hb) resume = nd.skip;
+      if (GENERAL && act && !hb) resume = nd.skip;
       i = __ballot(hb) ? i + 1 : nd.skip;
     }
-    if (!__ballot(resume != 0x7fffffff)) break;
   }
 #ifdef DT_STAMPS
   {   // walks whose active lanes all ended occluded (28 visits, 29 walks) / none occluded (30, 31)
