@@ -32,6 +32,8 @@ thread_local std::string g_err;
 struct HScene {
   const void* nodes;
   const void* fnodes;
+  const uint32_t* sg_cells;
+  const int32_t* sg_list;
   const int32_t* leaf_idx;
   const void* hdr;
   const double* geom;
@@ -93,6 +95,9 @@ struct dt_scene {
   void* d_nodes = nullptr;
   void* d_fnodes = nullptr;
   int n_fnodes = 0;
+  ShadowGrid sg;
+  void* d_sg_cells = nullptr;
+  void* d_sg_list = nullptr;
   int ftree_mode = 0;
   void* d_leaf = nullptr;
   void* d_hdr = nullptr;
@@ -214,6 +219,29 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
   if (!s->ftree_mode || !build_fast_tree(dnodes, fnodes)) fnodes.clear();
   s->n_fnodes = (int)fnodes.size();
   if (fnodes.empty()) fnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
+  // shadow grid (host_shadowgrid.cpp); DT_SHADOW_GRID=0: every shadow test walks a tree
+  const char* sgv = getenv("DT_SHADOW_GRID");
+  const char* sgc = getenv("DT_SG_CELLS");
+  const char* sgr = getenv("DT_SG_REACH");
+  if ((sgv && sgv[0] == '0') ||
+      !build_shadow_grid(dnodes, f.lights, s->sg, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : 0.5f))
+    s->sg = ShadowGrid();
+  if (getenv("DT_SG_VERBOSE")) {
+    size_t cells = s->sg.cells.size() / 2, tree = 0, sum = 0, mx = 0;
+    for (size_t c = 0; c < cells; ++c) {
+      const uint32_t n = s->sg.cells[2 * c + 1];
+      if (n == 0xffffffffu) { ++tree; continue; }
+      sum += n;
+      mx = std::max(mx, (size_t)n);
+    }
+    fprintf(stderr, "shadow grid: lights %d dim %dx%dx%d cells %zu (tree %zu) mean list %.2f max %zu list pool %zu\n",
+            s->sg.n_lights, s->sg.dim[0], s->sg.dim[1], s->sg.dim[2], cells, tree,
+            cells > tree ? (double)sum / (cells - tree) : 0.0, mx, s->sg.list.size());
+  }
+  if ((rc = upload(s->sg.cells, &s->d_sg_cells)) || (rc = upload(s->sg.list, &s->d_sg_list))) {
+    dt_scene_destroy(s);
+    return rc;
+  }
   if ((rc = upload(dnodes, &s->d_nodes)) || (rc = upload(fnodes, &s->d_fnodes)) || (rc = upload(leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
       (rc = upload(f.geom, &s->d_geom)) || (rc = upload(f.mat, &s->d_mat)) || (rc = upload(f.lights, &s->d_lights)) ||
       (rc = upload(f.tex, &s->d_tex))) {
@@ -235,7 +263,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
 void dt_scene_destroy(dt_scene* s)
 {
   if (!s) return;
-  void* bufs[] = {s->d_nodes, s->d_fnodes, s->d_leaf, s->d_hdr, s->d_geom, s->d_mat, s->d_lights, s->d_tex, s->d_zs,
+  void* bufs[] = {s->d_nodes, s->d_fnodes, s->d_sg_cells, s->d_sg_list, s->d_leaf, s->d_hdr, s->d_geom, s->d_mat, s->d_lights, s->d_tex, s->d_zs,
                   s->d_stats, s->d_launch};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -316,6 +344,14 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   P.n_nodes = (int32_t)sc->flat.bvh.nodes.size();
   P.n_fnodes = sc->n_fnodes;
   P.ftree_mode = sc->ftree_mode;
+  P.sg_n = sc->sg.n_lights;
+  for (int a = 0; a < 3; ++a) {
+    P.sg_dim[a] = sc->sg.dim[a];
+    P.sg_lo[a] = sc->sg.lo[a];
+    P.sg_inv[a] = sc->sg.inv_h[a];
+  }
+  for (int l = 0; l < DT_MAX_SGRID; ++l) P.sg_base[l] = sc->sg.base[l];
+  P.sg_reach = sc->sg.reach;
 
   P.n_lights = (int32_t)sc->flat.lights.size();
   P.n_shapes = (int32_t)sc->flat.hdr.size();
@@ -341,6 +377,8 @@ static int enqueue_render(dt_scene* sc, const dtd::DParams& P, const std::vector
   HScene hs;
   hs.nodes = sc->d_nodes;
   hs.fnodes = sc->d_fnodes;
+  hs.sg_cells = (const uint32_t*)sc->d_sg_cells;
+  hs.sg_list = (const int32_t*)sc->d_sg_list;
   hs.leaf_idx = (const int32_t*)sc->d_leaf;
   hs.hdr = sc->d_hdr;
   hs.geom = (const double*)sc->d_geom;

@@ -84,6 +84,8 @@ typedef const DT_CAS double* GP;
 struct DScene {
   const DNodeDev* nodes;    // the reference's tree (general walks)
   const DNodeDev* fnodes;   // same leaves, SAH inner nodes (host_fasttree.cpp; fast walks)
+  const uint32_t* sg_cells; // shadow grid (host_shadowgrid.cpp): (offset, count) per light x cell
+  const int32_t* sg_list;   // candidate occluder leaves (indices into nodes)
   const int32_t* leaf_idx;
   const DShapeHdr* hdr;
   const double* geom;
@@ -1054,6 +1056,38 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
   return any;
 }
 
+// intersectShadow over a gathered leaf's shapes for the lanes with `hb` (cpp:832-852)
+template <class CNT>
+__device__ __forceinline__ void shadow_leaf(const DScene& S, const DNodeDev& nd, bool hb, bool& occl, V3 sn, V3 sstart,
+                                            float t_max, int skip_shape, float shift, CNT& cnt)
+{
+  DT_T(q0);
+  const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
+  for (int q = 0; q < nq; ++q) {
+    int sid, type, off;
+    uint32_t flags;
+    leaf_shape(S, nd, q, sid, type, flags, off);
+    DT_CNT(8);
+    DT_CNT(18 + (type & 7));   // shadow prim tests by type (8 -> 18)
+    const bool test = hb && !occl && sid != skip_shape;
+    if (test) {
+      DT_WORK(cnt.prim++);
+#ifndef DT_ABL_NOPRIM_SHADOW
+      if (shape_shadow(type, flags, cas(S.geom) + off, sn, sstart, t_max, shift)) occl = true;
+#endif
+    }
+  }
+  DT_T(q1);
+  DT_ACC(32, q0, q1);
+}
+
+// an occluder at distance t' < t_max along sn from sstart sits at sray-parameter
+// u < 1 + 1e-3/|sray| from bstart; margins cover the f32 rounding
+__device__ __forceinline__ float shadow_tcull(float t_max)
+{
+  return t_max > 1e-3f ? (1.0f + 1e-3f / t_max) * 1.0001f + 1e-4f : FLT_MAX;
+}
+
 // any-hit shadow test (cpp:806-855): box test with sray from isectP+sray*1e-3, shape test
 // with normalized sray from isectP+sn*1e-3, skipping the light's own shape.
 template <bool GENERAL, class CNT>
@@ -1065,9 +1099,7 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
   const DNodeDev* const NODES = ftree ? S.fnodes : S.nodes;   // any-hit: order free
   int resume = active ? 0 : 0x7fffffff;
   bool occl = false;
-  // an occluder at distance t' < t_max along sn from sstart sits at sray-parameter
-  // u < 1 + 1e-3/|sray| from bstart; margins cover the f32 rounding
-  const float tcull = t_max > 1e-3f ? (1.0f + 1e-3f / t_max) * 1.0001f + 1e-4f : FLT_MAX;
+  const float tcull = shadow_tcull(t_max);
 #ifdef DT_ABL_NOSHADOW
   return false;
 #endif
@@ -1086,26 +1118,7 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
     ++nv;
 #endif
     if (nd.meta & DN_LEAF) {
-      if (__ballot(hb)) {
-        DT_T(q0);
-        const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
-        for (int q = 0; q < nq; ++q) {
-          int sid, type, off;
-          uint32_t flags;
-          leaf_shape(S, nd, q, sid, type, flags, off);
-          DT_CNT(8);
-          DT_CNT(18 + (type & 7));   // shadow prim tests by type (8 -> 18)
-          const bool test = hb && !occl && sid != skip_shape;
-          if (test) {
-            DT_WORK(cnt.prim++);
-#ifndef DT_ABL_NOPRIM_SHADOW
-            if (shape_shadow(type, flags, cas(S.geom) + off, sn, sstart, t_max, shift)) occl = true;
-#endif
-          }
-        }
-        DT_T(q1);
-        DT_ACC(32, q0, q1);
-      }
+      if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, shift, cnt);
       if (GENERAL) {
         if (act) resume = occl ? 0x7fffffff : nd.skip;
         if (!__ballot(resume != 0x7fffffff)) break;
@@ -1128,9 +1141,35 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
   return occl;
 }
 
+// The shadow test over a cell's candidate list (host_shadowgrid.cpp): the same box test and
+// shape tests as the walk, on the only leaves that can hold an occluder for this cell and light.
+template <class CNT>
+__device__ bool occluded_list(const DScene& S, const Walk& w, bool active, V3 bstart, V3 sn, V3 sstart, float t_max,
+                              int skip_shape, uint32_t off, uint32_t n, CNT& cnt)
+{
+  bool occl = false;
+  const float tcull = shadow_tcull(t_max);
+  for (uint32_t k = 0; k < n; ++k) {
+    const DNodeDev nd = cas(S.nodes)[cas(S.sg_list)[off + k]];
+    const bool hb = active & !occl & node_hit<false>(w, nd, 0.0f, bstart, tcull);
+    DT_CNT(34);
+    if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, 0.0f, cnt);
+    if (!__ballot(active & !occl)) break;
+  }
+  return occl;
+}
+
+// shading point in grid-cell coordinates
+__device__ __forceinline__ void sg_coords(const DParams& P, V3 p, float& x, float& y, float& z)
+{
+  x = ((float)p.x - P.sg_lo[0]) * P.sg_inv[0];
+  y = ((float)p.y - P.sg_lo[1]) * P.sg_inv[1];
+  z = ((float)p.z - P.sg_lo[2]) * P.sg_inv[2];
+}
+
 template <class CNT>
 __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
-                                         V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
+                                         V3 sstart, float t_max, int skip_shape, int li, float shift, CNT& cnt)
 {
   const Walk w = make_walk(active, sray, bstart, shift);
   if (w.inf_wave || w.bump_wave)
@@ -1138,6 +1177,35 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
 #ifdef DT_ABL_NOSHADOW
   return false;
 #endif
+  // Shadow grid: the first active lane's cell serves every lane within sg_reach cells of it.
+  // Waves whose lanes all lie within that reach (coherent primary bounces) test the cell's
+  // candidate list; scattered waves (a second union list measured no better) walk the tree.
+  if (li < P.sg_n && P.sg_base[li] >= 0) {
+    const unsigned long long am = __ballot(active);
+    if (!am) return false;
+    float x, y, z;
+    sg_coords(P, sstart, x, y, z);
+    const int first = (int)__builtin_ctzll(am);
+    const float x0 = floorf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), first)));
+    const float y0 = floorf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(y), first)));
+    const float z0 = floorf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(z), first)));
+    const bool inside = x0 >= 0.0f && y0 >= 0.0f && z0 >= 0.0f && x0 < (float)P.sg_dim[0] &&
+                        y0 < (float)P.sg_dim[1] && z0 < (float)P.sg_dim[2];
+    const float r = P.sg_reach;
+    const bool near = (x >= x0 - r) & (x <= x0 + 1.0f + r) & (y >= y0 - r) & (y <= y0 + 1.0f + r) &
+                      (z >= z0 - r) & (z <= z0 + 1.0f + r);
+    DT_CNT(inside ? 36 : 38);
+    if (inside && !__ballot(active & !near)) {
+      const int c0 = ((int)z0 * P.sg_dim[1] + (int)y0) * P.sg_dim[0] + (int)x0;
+      const DT_CAS uint32_t* e = cas(S.sg_cells) + 2 * (size_t)(P.sg_base[li] + c0);
+      const uint32_t off = e[0], n = e[1];
+      if (n != 0xffffffffu) {
+        DT_CNT(35);
+        return occluded_list(S, w, active, bstart, sn, sstart, t_max, skip_shape, off, n, cnt);
+      }
+      DT_CNT(37);
+    }
+  }
   return occluded_walk<false>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 }
 
@@ -1468,7 +1536,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
         }
         DT_T(t4);
         bool occl = occluded(S, P, walk, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
-                             t_max, L.shape_index, shift, cnt);
+                             t_max, L.shape_index, li, shift, cnt);
         DT_T(t5);
         DT_ACC(3, t4, t5);
         if (walk && !occl) vis |= 1u << li;

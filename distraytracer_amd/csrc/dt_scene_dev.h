@@ -93,6 +93,9 @@ enum { CK_R = 0, CK_GN = 14, CK_A = 17, CK_B = 20, CK_C = 23, CK_D = 26, CK_HOLE
        CK_COL1 = 44, CK_COL2 = 47, CK_COL = 50, CK_AD = 53, CK_DC = 56, CK_NADC = 59, CK_MUD = 60,
        CK_MVD = 61, CK_BW = 62, CK_SIZE = 63 };
 
+#define DT_MAX_SGRID 16        // lights with a shadow grid (host_shadowgrid.cpp)
+#define DT_SGRID_MAX_LIST 48   // longer candidate lists: the cell walks the tree instead
+
 // per-render constants (kernel argument, < 4 KB)
 struct DParams {
   int32_t xRes, yRes;
@@ -105,6 +108,11 @@ struct DParams {
   int32_t reflect, nogloss, perlin_cloud;
   int32_t n_nodes, n_lights, n_shapes;
   int32_t n_fnodes;       // fast tree (host_fasttree.cpp); 0: every wave walks the reference tree
+  int32_t sg_n;           // shadow grid: lights 0..sg_n-1 (sg_base < 0: none for that light)
+  int32_t sg_dim[3];
+  int32_t sg_base[DT_MAX_SGRID];
+  float sg_lo[3], sg_inv[3];
+  float sg_reach;         // a cell's list also covers points this many cells outside it
   int32_t ftree_mode;     // walks that use it: bit 0 closest hit, bit 1 shadow
   int32_t n_cloud_steps;
   uint32_t seed;

@@ -21,6 +21,19 @@ void build_bvh(const dt_scene_desc& d, const dt_globals& g, FlatBVH& out);
 // host_fasttree.cpp: same leaves, SAH inner nodes, 16-bit leaf ranks in meta (false: no fast tree)
 bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNodeDev>& out);
 
+// host_shadowgrid.cpp: per-light candidate-occluder lists per grid cell (false: no grid)
+struct ShadowGrid {
+  int n_lights = 0;                  // lights 0..n_lights-1 (base[l] < 0: that light has none)
+  int32_t base[DT_MAX_SGRID] = {};   // first cell record of light l in `cells`
+  int dim[3] = {0, 0, 0};
+  float lo[3] = {0, 0, 0}, inv_h[3] = {0, 0, 0};
+  float reach = 0.5f;                // a cell's list covers points this many cells outside it
+  std::vector<uint32_t> cells;       // (offset into list, count | 0xffffffff: walk the tree) per cell
+  std::vector<int32_t> list;         // leaf node indices (reference tree)
+};
+bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const std::vector<dtd::DLight>& lights,
+                       ShadowGrid& g, double target_cells = 32768, float reach = 0.5f);
+
 // device-layout scene produced from a descriptor (host_flatten.cpp)
 struct FlatScene {
   FlatBVH bvh;

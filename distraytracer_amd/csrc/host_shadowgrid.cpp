@@ -1,0 +1,151 @@
+// host_shadowgrid.cpp — per-light candidate-occluder lists over a uniform grid of shading-point
+// cells, for the shadow test (render_final_project.cpp:806-855).
+//
+// The reference decides a shadow ray by gathering every leaf whose box the ray passes and
+// testing each leaf's shapes with intersectShadow. Only a shape hit at distance t < t_max along
+// the segment from isectP + 1e-3·sn counts, and every shape lies inside its leaf box with 1e-2 to
+// spare (BoundingVolume pads its bounds, geometry.cpp:2632-2655). For a point or rectangle light
+// the segment ends on the light, so a segment starting in cell C lies in the box hull of C and the
+// light (C widened by the reach below). A leaf whose box misses that hull cannot occlude any
+// segment from C, whatever the
+// rounding of the reference's tests (1e-6 relative, far inside the margins below). Each list holds
+// the leaves whose box meets the hull. The device tests exactly those leaves (box test, then the
+// shapes), which answers as the full gather does. Sphere lights are excluded: their sampleRay
+// returns the sampled point itself (Q11), so the "segment" does not end on the light.
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <vector>
+
+#include "host_internal.h"
+
+namespace dth {
+
+namespace {
+
+// cells i in [0, n) whose interval [lo + i h - m, lo + (i+1) h + m], joined with the light
+// interval [llo, lhi], meets the leaf interval [a, b]
+void cell_range(double lo, double h, int n, double m, double llo, double lhi, double a, double b, int& i0,
+                int& i1)
+{
+  // hull interval: [min(cell_lo, llo), max(cell_hi, lhi)]; meets [a, b] iff
+  // min(cell_lo, llo) <= b and max(cell_hi, lhi) >= a
+  i0 = 0;
+  i1 = n - 1;
+  if (llo > b) {   // need cell_lo = lo + i h - m <= b
+    const double lim = std::floor((b + m - lo) / h);
+    i1 = std::min(i1, (int)std::max(-1.0, std::min((double)n, lim)));
+  }
+  if (lhi < a) {   // need cell_hi = lo + (i+1) h + m >= a
+    const double lim = std::ceil((a - m - lo) / h - 1);
+    i0 = std::max(i0, (int)std::min((double)n, std::max(-1.0, lim)));
+  }
+}
+
+}  // namespace
+
+bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const std::vector<dtd::DLight>& lights,
+                       ShadowGrid& g, double target_cells, float reach)
+{
+  g = ShadowGrid();
+  g.reach = reach;
+  if (nodes.empty() || !(nodes[0].lb[0] <= nodes[0].ub[0])) return false;
+  std::vector<int> leaves;
+  for (size_t i = 0; i < nodes.size(); ++i)
+    if (nodes[i].meta & dtd::DN_LEAF) leaves.push_back((int)i);
+  if (leaves.empty()) return false;
+  // Grid box: where the shading points are. A few giant shapes (C3's window-frame prisms span
+  // y in [-996, 1004]) would stretch a box around everything into useless slabs, so per axis
+  // take the union of the 90% shortest leaf intervals, widened by half its size, within the
+  // root box. Points outside the grid walk the tree.
+  double lo[3], ext[3], vol = 1;
+  for (int a = 0; a < 3; ++a) {
+    std::vector<double> e;
+    for (int l : leaves) e.push_back(nodes[l].ub[a] - nodes[l].lb[a]);
+    std::sort(e.begin(), e.end());
+    const double thr = e[std::min(e.size() - 1, (size_t)(0.9 * (double)e.size()))];
+    double c0 = INFINITY, c1 = -INFINITY;
+    for (int l : leaves)
+      if (nodes[l].ub[a] - nodes[l].lb[a] <= thr) {
+        c0 = std::min(c0, nodes[l].lb[a]);
+        c1 = std::max(c1, nodes[l].ub[a]);
+      }
+    const double w = c1 - c0;
+    c0 = std::max(c0 - 0.5 * w, nodes[0].lb[a]);
+    c1 = std::min(c1 + 0.5 * w, nodes[0].ub[a]);
+    if (!(c1 > c0)) return false;
+    lo[a] = c0;
+    ext[a] = std::max(c1 - c0, 1e-3);
+    vol *= ext[a];
+  }
+  if (!std::isfinite(vol) || vol <= 0) return false;
+  const double h = std::cbrt(vol / target_cells);
+  double hh[3];
+  for (int a = 0; a < 3; ++a) {
+    g.dim[a] = std::max(1, std::min(256, (int)std::ceil(ext[a] / h)));
+    hh[a] = ext[a] / g.dim[a];
+    g.lo[a] = (float)lo[a];
+    g.inv_h[a] = (float)(1.0 / hh[a]);
+  }
+  const int ncell = g.dim[0] * g.dim[1] * g.dim[2];
+  // margins: a cell's list serves every shading point within `reach` cells of it (the
+  // device checks that reach per lane), plus slack for the f32 cell coordinates (m1); the
+  // segment ends 1e-3 past the light sample (m2)
+  double scale = 0;
+  for (int a = 0; a < 3; ++a) scale = std::max({scale, std::fabs(lo[a]), std::fabs(lo[a] + ext[a])});
+  const double m1 = (reach + 0.05) * std::max({hh[0], hh[1], hh[2]}) + 1e-4 * (1 + scale);
+  const double m2 = 2e-3 + 1e-4 * (1 + scale);
+
+  std::map<std::vector<int32_t>, uint32_t> uniq;
+  std::vector<std::vector<int32_t>> lists(ncell);
+  for (size_t l = 0; l < lights.size() && l < (size_t)DT_MAX_SGRID; ++l) {
+    const dtd::DLight& L = lights[l];
+    g.base[l] = -1;
+    if (L.type != DT_LIGHT_POINT && L.type != DT_LIGHT_RECT) continue;
+    double llo[3], lhi[3];
+    for (int a = 0; a < 3; ++a) {
+      if (L.type == DT_LIGHT_POINT) {
+        llo[a] = lhi[a] = L.center[a];
+      } else {   // parallelogram A, B, B + D - A, D (rect_sample stays inside it)
+        const double c = L.B[a] + L.D[a] - L.A[a];
+        llo[a] = std::min({L.A[a], L.B[a], L.D[a], c});
+        lhi[a] = std::max({L.A[a], L.B[a], L.D[a], c});
+      }
+      llo[a] -= m2;
+      lhi[a] += m2;
+    }
+    for (auto& v : lists) v.clear();
+    for (int leaf : leaves) {
+      const dtd::DNodeDev& nd = nodes[leaf];
+      int r0[3], r1[3];
+      for (int a = 0; a < 3; ++a) cell_range(lo[a], hh[a], g.dim[a], m1, llo[a], lhi[a], nd.lb[a], nd.ub[a], r0[a], r1[a]);
+      for (int z = r0[2]; z <= r1[2]; ++z)
+        for (int y = r0[1]; y <= r1[1]; ++y)
+          for (int x = r0[0]; x <= r1[0]; ++x) lists[(z * g.dim[1] + y) * g.dim[0] + x].push_back(leaf);
+    }
+    g.base[l] = (int32_t)g.cells.size() / 2;
+    for (int c = 0; c < ncell; ++c) {
+      std::vector<int32_t>& v = lists[c];
+      if ((int)v.size() > DT_SGRID_MAX_LIST) {   // the tree walk is cheaper for long lists
+        g.cells.push_back(0);
+        g.cells.push_back(0xffffffffu);
+        continue;
+      }
+      auto it = uniq.find(v);
+      uint32_t off;
+      if (it == uniq.end()) {
+        off = (uint32_t)g.list.size();
+        g.list.insert(g.list.end(), v.begin(), v.end());
+        uniq.emplace(v, off);
+      } else {
+        off = it->second;
+      }
+      g.cells.push_back(off);
+      g.cells.push_back((uint32_t)v.size());
+    }
+    g.n_lights = (int)l + 1;
+  }
+  return g.n_lights > 0;
+}
+
+}  // namespace dth

@@ -213,6 +213,26 @@ def test_fast_tree_gathers_the_reference_leaves(cuda, monkeypatch):
         assert np.array_equal(fast_img, ref_img), mode
 
 
+def test_shadow_grid_matches_tree_walks(cuda, monkeypatch):
+    """The shadow grid (host_shadowgrid.cpp: per-light candidate-occluder lists per cell) must
+    answer every shadow ray as the tree walk does: C3-like window (64 spp, depth 8, DoF, glossy
+    floor, 4 area lights + the window point light) with and without it, bit for bit."""
+    g = dt.globals_default()
+    g.use_model = 0
+    built = dt.build_scene("final", 240, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.brdf_samples = 1920, 1080, 64, 8, 2
+    tile = dt.tiles(x0=900, y0=500, x1=964, y1=548)
+    monkeypatch.setenv("DT_SHADOW_GRID", "0")
+    ref_img, ref_st = _render_gpu(built, g, 240, tile)
+    for cells, reach in (("32768", "0.5"), ("4096", "2")):
+        monkeypatch.setenv("DT_SHADOW_GRID", "1")
+        monkeypatch.setenv("DT_SG_CELLS", cells)
+        monkeypatch.setenv("DT_SG_REACH", reach)
+        img, st = _render_gpu(built, g, 240, tile)
+        assert st.shadow_rays == ref_st.shadow_rays
+        assert np.array_equal(img, ref_img), (cells, reach)
+
+
 def _feature_scene():
     """A synthetic scene for the shading paths the shipped builders never use: a glass sphere
     (refraction + Fresnel, Q5), a steel mirror sphere, an Oren-Nayar sphere, a raw triangle, a
