@@ -53,7 +53,9 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const std::vecto
   std::vector<int> leaves;
   for (size_t i = 0; i < nodes.size(); ++i)
     if (nodes[i].meta & dtd::DN_LEAF) leaves.push_back((int)i);
-  if (leaves.empty()) return false;
+  // large leaf counts (meshes): the per-leaf cell ranges would cost seconds of host time per
+  // scene and the lists would overflow anyway; such scenes walk the tree
+  if (leaves.empty() || leaves.size() > 4096) return false;
   // Grid box: where the shading points are. A few giant shapes (C3's window-frame prisms span
   // y in [-996, 1004]) would stretch a box around everything into useless slabs, so per axis
   // take the union of the 90% shortest leaf intervals, widened by half its size, within the
