@@ -379,8 +379,9 @@ __device__ __forceinline__ V3 v3a(GP a) { return v3(a[0], a[1], a[2]); }
 __device__ __forceinline__ V3 G3(GP g, int o) { return v3(g[o], g[o + 1], g[o + 2]); }
 
 // Rectangle plane + quad bounds test (geometry.cpp:640-741 / 2292-2312): R record
+// tlim: the caller discards t >= tlim (shadow tests: t_max), so such planes may be rejected early
 __device__ __forceinline__ bool rect_hit_R(GP R, V3 ray, V3 start, float eps,
-                                           float& t_out, float& ch1, float& ch2)
+                                           float& t_out, float& ch1, float& ch2, float tlim = INFINITY)
 {
   V3 A = G3(R, R_A), n = G3(R, R_N);
   float dn = (float)dot(ray, n);
@@ -389,6 +390,13 @@ __device__ __forceinline__ bool rect_hit_R(GP R, V3 ray, V3 start, float eps,
   // t = num/dn <= 0 < eps whenever the signs differ or num is 0: reject before the f64
   // division (identical outcome; a NaN num still reaches the division and fails below)
   if ((num > 0) != (dn > 0) && !(num != num)) return false;
+  // |num| >= |dn| tlim (1 + 2^-20) puts num/dn, and its f32 rounding, at or past tlim;
+  // |num| <= |dn| eps (1 - 2^-20) puts it at or below eps: both decided without the division
+  {
+    const double an = fabs(num), ad = fabs((double)dn);
+    if (an >= ad * (double)tlim * (1.0 + 0x1p-20)) return false;
+    if (an <= ad * (double)eps * (1.0 - 0x1p-20)) return false;
+  }
   float t_final = (float)(num / dn);
   if (t_final <= eps) return false;
   V3 point = add(start, mul(t_final, ray));
@@ -655,17 +663,17 @@ __device__ bool shape_shadow(int type, uint32_t flags, GP g, V3 ray, V3 start,
         shifted_rect(g, shift, A, B, C, D);
         return rect_hit_raw(A, B, C, D, ray, start, 1e-4f, tt) && tt < t_max;
       }
-      return rect_hit_R(g + RC_R, ray, start, 1e-4f, tt, a, b) && tt < t_max;
+      return rect_hit_R(g + RC_R, ray, start, 1e-4f, tt, a, b, t_max) && tt < t_max;
     case DT_SHAPE_CHECKERBOARD:
-      return rect_hit_R(g + CK_R, ray, start, 1e-4f, tt, a, b) && tt < t_max;
+      return rect_hit_R(g + CK_R, ray, start, 1e-4f, tt, a, b, t_max) && tt < t_max;
     case DT_SHAPE_RECTPRISM_V2:
 #pragma unroll 1
       for (int f = 0; f < 6; ++f)
-        if (rect_hit_R(g + PR_F + f * R_SIZE, ray, start, 1e-4f, tt, a, b) && tt < t_max) return true;
+        if (rect_hit_R(g + PR_F + f * R_SIZE, ray, start, 1e-4f, tt, a, b, t_max) && tt < t_max) return true;
       return false;
     case DT_SHAPE_CHECKERBOARD_HOLE:
-      if (rect_hit_R(g + CK_R, ray, start, 1e-3f, tt, a, b) && tt < t_max) {
-        if (rect_hit_R(g + CK_HOLE, ray, start, 1e-4f, tt, a, b) && tt < t_max) return false;
+      if (rect_hit_R(g + CK_R, ray, start, 1e-3f, tt, a, b, t_max) && tt < t_max) {
+        if (rect_hit_R(g + CK_HOLE, ray, start, 1e-4f, tt, a, b, t_max) && tt < t_max) return false;
         return true;
       }
       return false;

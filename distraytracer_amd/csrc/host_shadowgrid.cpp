@@ -5,8 +5,8 @@
 // testing each leaf's shapes with intersectShadow. Only a shape hit at distance t < t_max along
 // the segment from isectP + 1e-3·sn counts, and every shape lies inside its leaf box with 1e-2 to
 // spare (BoundingVolume pads its bounds, geometry.cpp:2632-2655). For a point or rectangle light
-// the segment ends on the light, so a segment starting in cell C lies in the box hull of C and the
-// light (C widened by the reach below). A leaf whose box misses that hull cannot occlude any
+// the segment ends on the light, so a segment starting in cell C lies in the swept box between C
+// (widened by the reach below) and the light's box. A leaf whose box misses it cannot occlude any
 // segment from C, whatever the
 // rounding of the reference's tests (1e-6 relative, far inside the margins below). Each list holds
 // the leaves whose box meets the hull. The device tests exactly those leaves (box test, then the
@@ -40,6 +40,31 @@ void cell_range(double lo, double h, int n, double m, double llo, double lhi, do
     const double lim = std::ceil((a - m - lo) / h - 1);
     i0 = std::max(i0, (int)std::min((double)n, std::max(-1.0, lim)));
   }
+}
+
+// Does some segment from box C to box L meet box B? Every such segment lies in the swept box
+// {(1-t) C + t L : t in [0,1]} (per axis an interval whose ends move linearly in t), which is
+// tighter than the box hull of C and L for oblique cells. Per axis the overlap condition is two
+// linear inequalities in t; the test passes iff their solution sets meet in [0, 1].
+bool swept_meets(const double clo[3], const double chi[3], const double llo[3], const double lhi[3],
+                 const double* blo, const double* bhi)
+{
+  double t0 = 0, t1 = 1;
+  const double slack = 1e-9;
+  for (int a = 0; a < 3; ++a) {
+    // lower end clo + t (llo - clo) <= bhi
+    const double d0 = llo[a] - clo[a], r0 = bhi[a] - clo[a];
+    if (d0 > 0) t1 = std::min(t1, r0 / d0 + slack);
+    else if (d0 < 0) t0 = std::max(t0, r0 / d0 - slack);
+    else if (r0 < 0) return false;
+    // upper end chi + t (lhi - chi) >= blo
+    const double d1 = lhi[a] - chi[a], r1 = blo[a] - chi[a];
+    if (d1 < 0) t1 = std::min(t1, r1 / d1 + slack);
+    else if (d1 > 0) t0 = std::max(t0, r1 / d1 - slack);
+    else if (r1 > 0) return false;
+    if (t0 > t1) return false;
+  }
+  return true;
 }
 
 }  // namespace
@@ -123,7 +148,15 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const std::vecto
       for (int a = 0; a < 3; ++a) cell_range(lo[a], hh[a], g.dim[a], m1, llo[a], lhi[a], nd.lb[a], nd.ub[a], r0[a], r1[a]);
       for (int z = r0[2]; z <= r1[2]; ++z)
         for (int y = r0[1]; y <= r1[1]; ++y)
-          for (int x = r0[0]; x <= r1[0]; ++x) lists[(z * g.dim[1] + y) * g.dim[0] + x].push_back(leaf);
+          for (int x = r0[0]; x <= r1[0]; ++x) {
+            const int ci[3] = {x, y, z};
+            double clo[3], chi[3];
+            for (int a = 0; a < 3; ++a) {
+              clo[a] = lo[a] + ci[a] * hh[a] - m1;
+              chi[a] = lo[a] + (ci[a] + 1) * hh[a] + m1;
+            }
+            if (swept_meets(clo, chi, llo, lhi, nd.lb, nd.ub)) lists[(z * g.dim[1] + y) * g.dim[0] + x].push_back(leaf);
+          }
     }
     g.base[l] = (int32_t)g.cells.size() / 2;
     for (int c = 0; c < ncell; ++c) {
