@@ -99,6 +99,7 @@ struct dt_scene {
   void* d_sg_cells = nullptr;
   void* d_sg_list = nullptr;
   int ftree_mode = 0;
+  int boxes_ordered = 0;   // lb <= ub on every axis of every node (both trees), no NaN bound
   void* d_leaf = nullptr;
   void* d_hdr = nullptr;
   void* d_geom = nullptr;
@@ -218,6 +219,11 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
   s->ftree_mode = !ft ? 1 : ft[0] == '1' ? 3 : ft[0] == 'c' ? 1 : ft[0] == 's' ? 2 : 0;
   if (!s->ftree_mode || !build_fast_tree(dnodes, fnodes)) fnodes.clear();
   s->n_fnodes = (int)fnodes.size();
+  s->boxes_ordered = 1;
+  for (const auto* v : {&dnodes, &fnodes})
+    for (const dtd::DNodeDev& n : *v)
+      for (int a = 0; a < 3; ++a)
+        if (!(n.lb[a] <= n.ub[a])) s->boxes_ordered = 0;
   if (fnodes.empty()) fnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
   // shadow grid (host_shadowgrid.cpp); DT_SHADOW_GRID=0: every shadow test walks a tree
   const char* sgv = getenv("DT_SHADOW_GRID");
@@ -344,6 +350,7 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   P.n_nodes = (int32_t)sc->flat.bvh.nodes.size();
   P.n_fnodes = sc->n_fnodes;
   P.ftree_mode = sc->ftree_mode;
+  P.boxes_ordered = sc->boxes_ordered;
   P.sg_n = sc->sg.n_lights;
   for (int a = 0; a < 3; ++a) {
     P.sg_dim[a] = sc->sg.dim[a];

@@ -55,6 +55,15 @@ using namespace dtd;
 #define DT_MAX_CLOUD_STEPS 2048
 #define DT_CLOUD_CHUNK 256
 #define DT_WAVE 64
+#ifndef DT_SLAB_MINMAX
+#define DT_SLAB_MINMAX 0   // min/max slab ends: exact, but measured 2% slower (register allocation)
+#endif
+#ifndef DT_TCULL_HOIST
+#define DT_TCULL_HOIST 1
+#endif
+#ifndef DT_LS_CACHE
+#define DT_LS_CACHE 4   // lights whose area-sample pair is kept in LDS between the two light passes
+#endif
 
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
        ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15, ST_N = 16 };
@@ -895,8 +904,17 @@ __device__ __forceinline__ bool box_hit_exact_finite(const DNodeDev& b, const Ra
   // (tx_min <= ty_max, ty_min <= tx_max, max(..) <= tz_max, tz_min <= min(..)) and the
   // final exit > 0: i.e. max3(entries) <= min3(exits) && min3(exits) > 0. No NaN can occur
   // here (finite inverse), and +-0 compare equal, so the min/max form decides identically.
+  // The entry of an axis is min(a, c) and its exit max(a, c): with lb <= ub (checked on the
+  // host for every node, P.boxes_ordered, else every wave takes the general test) rounding is
+  // monotone, so a <= c for inv > 0 and c <= a for inv < 0 -- the sign select of the
+  // reference, without per-ray sign masks held in SGPRs across the walk.
+#if DT_SLAB_MINMAX
+  const float tmin = fmaxf(fmaxf(fminf(ax, cx), fminf(ay, cy)), fminf(az, cz));
+  const float tmax = fminf(fminf(fmaxf(ax, cx), fmaxf(ay, cy)), fmaxf(az, cz));
+#else
   const float tmin = fmaxf(fmaxf(r.nx ? cx : ax, r.ny ? cy : ay), r.nz ? cz : az);
   const float tmax = fminf(fminf(r.nx ? ax : cx, r.ny ? ay : cy), r.nz ? az : cz);
+#endif
   return (tmin <= tmax) & (tmax > 0) & (tmin <= tcull);
 }
 
@@ -924,13 +942,13 @@ struct Walk {
 
 // inf_wave also takes NaN rays/origins: the reference's slab sequence treats a NaN axis
 // asymmetrically (x fails, y/z are skipped), which only the exact general test reproduces.
-__device__ __forceinline__ Walk make_walk(bool active, V3 ray, V3 st, float shift)
+__device__ __forceinline__ Walk make_walk(const DParams& P, bool active, V3 ray, V3 st, float shift)
 {
   Walk w;
   w.rb = make_raybox(ray);
   const bool odd = w.rb.ix | w.rb.iy | w.rb.iz | isnan(ray.x) | isnan(ray.y) | isnan(ray.z) | isnan(st.x) |
                    isnan(st.y) | isnan(st.z);
-  w.inf_wave = __ballot(active && odd) != 0;
+  w.inf_wave = __ballot(active && odd) != 0 || (DT_SLAB_MINMAX && !P.boxes_ordered);
   w.bump_wave = __ballot(active && shift != 0.0f) != 0;
   return w;
 }
@@ -988,6 +1006,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
   const DNodeDev* const NODES = ftree ? S.fnodes : S.nodes;
   int resume = active ? 0 : 0x7fffffff;
   float t_dist = FLT_MAX;
+  float tcull = FLT_MAX;   // culling bound from the best hit so far (updated with it)
   bool any = false;
   h.t_min = FLT_MAX;
   h.shape = -1;
@@ -1003,7 +1022,9 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
     // finite-ray slab test (with the shrinking tcull) is monotone in the box, so a lane that
     // failed an ancestor fails here too (host_fasttree.cpp)
     const bool act = GENERAL ? resume <= i : active;
-    const float tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
+#if !DT_TCULL_HOIST
+    tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
+#endif
     const bool hb = act & node_hit<GENERAL>(w, nd, shift, org, tcull);
     DT_WORK(cnt.wnodes++; cnt.box += act);
     DT_CNT(26);
@@ -1031,6 +1052,9 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
                 h.shape = sid;
                 h.inside = ins;
                 h.t_min = t_dist;
+#if DT_TCULL_HOIST
+                tcull = t_dist == FLT_MAX ? FLT_MAX : t_dist * 1.0001f + 1e-4f;
+#endif
                 h.has_ccol = hc;
                 if (hc) h.ccol = cc;
               }
@@ -1054,7 +1078,7 @@ template <class CNT>
 __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 ray, V3 org, float shift,
                                             HitRec& h, CNT& cnt)
 {
-  const Walk w = make_walk(active, ray, org, shift);
+  const Walk w = make_walk(P, active, ray, org, shift);
   if (w.inf_wave || w.bump_wave) return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
   const bool any = closest_hit_walk<false>(S, P, w, active, ray, org, shift, h, cnt);
   // an edge-on checkerboard hit keeps the previous test's t (Q16): only the reference order
@@ -1179,7 +1203,7 @@ template <class CNT>
 __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
                                          V3 sstart, float t_max, int skip_shape, int li, float shift, CNT& cnt)
 {
-  const Walk w = make_walk(active, sray, bstart, shift);
+  const Walk w = make_walk(P, active, sray, bstart, shift);
   if (w.inf_wave || w.bump_wave)
     return occluded_walk<true>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 #ifdef DT_ABL_NOSHADOW
@@ -1274,21 +1298,35 @@ __device__ void glossy_rect(V3 refl_ray, V3 isectP, float mult, V3& A, V3& B, V3
   D = sub(A, mul(width, wv));
 }
 
+__device__ __forceinline__ V3 rect_sample_f(V3 A, V3 B, V3 D, float x, float y)
+{
+  return add(add(A, mul(x, sub(B, A))), mul(y, sub(D, A)));
+}
 __device__ __forceinline__ V3 rect_sample(V3 A, V3 B, V3 D, double u0, double u1)
 {
-  float x = (float)u0, y = (float)u1;
-  return add(add(A, mul(x, sub(B, A))), mul(y, sub(D, A)));
+  return rect_sample_f(A, B, D, (float)u0, (float)u1);
 }
 
 // light sampleRay (geometry.cpp:2751-2849)
+// xy: the area-light sample's float pair (rect_sample's (float)U draws). cache_mode 1 stores the
+// drawn pair there, 2 reuses the stored pair instead of drawing it again (same values).
 __device__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L, int li, V3 point, uint32_t node,
-                           unsigned long long* st_sphl)
+                           unsigned long long* st_sphl, float* xy = nullptr, int cache_mode = 0)
 {
   if (L.type == DT_LIGHT_POINT) return sub(v3a(L.center), point);
   if (L.type == DT_LIGHT_RECT) {
-    double u0, u1;
-    c.rng.draw(node, P_LIGHT, (uint32_t)li, u0, u1);
-    return sub(rect_sample(v3a(L.A), v3a(L.B), v3a(L.D), u0, u1), point);
+    float x, y;
+    if (cache_mode == 2) {
+      x = xy[0];
+      y = xy[DT_WAVE];
+    } else {
+      double u0, u1;
+      c.rng.draw(node, P_LIGHT, (uint32_t)li, u0, u1);
+      x = (float)u0;
+      y = (float)u1;
+      if (cache_mode == 1) { xy[0] = x; xy[DT_WAVE] = y; }
+    }
+    return sub(rect_sample_f(v3a(L.A), v3a(L.B), v3a(L.D), x, y), point);
   }
   V3 C = v3a(L.center), baxis = v3a(L.baxis);
   int attempt = 0;
@@ -1327,7 +1365,7 @@ __device__ __forceinline__ float schlick_complex(float cos_theta, double r0, dou
 // reference's accumulation order.
 __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t rootkey, float shift,
                          PassOut& out, Entry* stack, Counters& cnt, double (*nrec)[DT_WAVE],
-                         double (*ocol)[DT_WAVE])
+                         double (*ocol)[DT_WAVE], float (*lsxy)[2][DT_WAVE])
 {
   const DScene& S = *c.S;
   const DParams& P = *c.P;
@@ -1537,7 +1575,10 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
         float t_max = 0;
         V3 sn = v3(1, 0, 0);
         if (walk) {
-          sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL);
+          // the first DT_LS_CACHE area lights park their sample pair in LDS for pass 2
+          const bool cache = li < DT_LS_CACHE;
+          sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL, cache ? &lsxy[cache ? li : 0][0][ln_] : nullptr,
+                              cache ? 1 : 0);
           t_max = (float)norm(sray);
           sn = normalized(sray);
           cnt.shadow++;
@@ -1581,7 +1622,9 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           if (!(vis & (1u << li))) continue;
           const DT_CAS DLight& L = cas(S.lights)[li];
           const DMat& M = *Mp;
-          const V3 sray = light_sample(c, L, li, isectP, node, nullptr);
+          const bool cache = li < DT_LS_CACHE;
+          const V3 sray = light_sample(c, L, li, isectP, node, nullptr, cache ? &lsxy[cache ? li : 0][0][ln_] : nullptr,
+                                       cache ? 2 : 0);
           const V3 sn = normalized(sray);
           const V3 normal = nrm;
           V3 lc = v3a(L.color);
@@ -1737,6 +1780,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   __shared__ double ocol[3][DT_WAVE];
   __shared__ double psum[3][DT_WAVE];
   __shared__ double chan[4];
+  __shared__ float lsxy[DT_LS_CACHE > 0 ? DT_LS_CACHE : 1][2][DT_WAVE];
   __shared__ unsigned long long item_s;
   Entry stack[DT_STACK_MAX];
   const int lane = threadIdx.x;
@@ -1809,7 +1853,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         ocol[0][lane] = 0; ocol[1][lane] = 0; ocol[2][lane] = 0;
         po.hit = pass > 0;
         po.in_motion = false;
-        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt, nrec, ocol);
+        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt, nrec, ocol, lsxy);
         po.color = v3(ocol[0][lane], ocol[1][lane], ocol[2][lane]);
         if (pass == 0) {
           tmp_color = po.color;

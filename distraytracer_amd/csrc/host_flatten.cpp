@@ -58,6 +58,10 @@ int flatten_scene(const dt_scene_desc& d, const dt_globals& g, FlatScene& out, s
     err = "invalid scene descriptor";
     return DT_E_INVALID;
   }
+  if (d.n_lights > 32) {   // the device keeps one visibility bit per light in a 32-bit mask
+    err = "more than 32 lights";
+    return DT_E_LIMIT;
+  }
   // textures
   std::vector<int64_t> tex_off(d.n_textures);
   for (int i = 0; i < d.n_textures; ++i) {
