@@ -82,24 +82,37 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const std::vecto
   // scene and the lists would overflow anyway; such scenes walk the tree
   if (leaves.empty() || leaves.size() > 4096) return false;
   // Grid box: where the shading points are. A few giant shapes (C3's window-frame prisms span
-  // y in [-996, 1004]) would stretch a box around everything into useless slabs, so per axis
-  // take the union of the 90% shortest leaf intervals, widened by half its size, within the
-  // root box. Points outside the grid walk the tree.
+  // y in [-996, 1004]) would stretch a box around everything into useless slabs. Per axis the
+  // box is the hull of
+  //  * the union of the 90% shortest leaf intervals, widened by half its size (where most
+  //    shapes are), and
+  //  * the union of all leaf intervals but the few giant ones: the fewest longest leaves
+  //    (at most max(4, 10%)) whose removal shrinks the union at least 4x (the room; with
+  //    thousands of small mesh triangles the first term alone would shrink onto the meshes),
+  // within the root box. Points outside the grid walk the tree.
   double lo[3], ext[3], vol = 1;
   for (int a = 0; a < 3; ++a) {
-    std::vector<double> e;
-    for (int l : leaves) e.push_back(nodes[l].ub[a] - nodes[l].lb[a]);
-    std::sort(e.begin(), e.end());
-    const double thr = e[std::min(e.size() - 1, (size_t)(0.9 * (double)e.size()))];
-    double c0 = INFINITY, c1 = -INFINITY;
-    for (int l : leaves)
-      if (nodes[l].ub[a] - nodes[l].lb[a] <= thr) {
-        c0 = std::min(c0, nodes[l].lb[a]);
-        c1 = std::max(c1, nodes[l].ub[a]);
-      }
+    std::vector<std::pair<double, int>> byext;
+    for (int l : leaves) byext.push_back({nodes[l].ub[a] - nodes[l].lb[a], l});
+    std::sort(byext.begin(), byext.end());
+    const size_t n = byext.size();
+    // plo/phi[k]: union of the k shortest leaf intervals
+    std::vector<double> plo(n + 1, INFINITY), phi(n + 1, -INFINITY);
+    for (size_t k = 0; k < n; ++k) {
+      plo[k + 1] = std::min(plo[k], nodes[byext[k].second].lb[a]);
+      phi[k + 1] = std::max(phi[k], nodes[byext[k].second].ub[a]);
+    }
+    const size_t k90 = std::max((size_t)1, std::min(n, (size_t)(0.9 * (double)n) + 1));
+    double c0 = plo[k90], c1 = phi[k90];
     const double w = c1 - c0;
-    c0 = std::max(c0 - 0.5 * w, nodes[0].lb[a]);
-    c1 = std::min(c1 + 0.5 * w, nodes[0].ub[a]);
+    c0 -= 0.5 * w;
+    c1 += 0.5 * w;
+    size_t keep = n;
+    const size_t max_drop = std::max((size_t)4, n / 10);
+    for (size_t k = n - 1; k >= 1 && n - k <= max_drop; --k)
+      if (phi[n] - plo[n] > 4.0 * (phi[k] - plo[k])) { keep = k; break; }
+    c0 = std::max(std::min(c0, plo[keep]), nodes[0].lb[a]);
+    c1 = std::min(std::max(c1, phi[keep]), nodes[0].ub[a]);
     if (!(c1 > c0)) return false;
     lo[a] = c0;
     ext[a] = std::max(c1 - c0, 1e-3);

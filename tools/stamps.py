@@ -13,10 +13,12 @@ NAMES = ["pop", "closest_hit", "hit+children", "occluded", "light loop rest", "s
 
 
 def main():
+    # config: c3 (default) or c4 (use_model, 256 spp)
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
     g = dt.globals_default()
-    g.use_model = 0
+    g.use_model = 1 if cfg == "c4" else 0
     b = dt.build_scene("final", 240, g)
-    g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.brdf_samples = 1920, 1080, 64, 8, 2
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.brdf_samples = 1920, 1080, 256 if cfg == "c4" else 64, 8, 2
     s = dt.Scene(b, g)
     out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
     st = dt.render(s, g, 240, out)
@@ -26,7 +28,7 @@ def main():
     print("kernel ms %.2f" % st.kernel_ms)
     for i, n in enumerate(NAMES[:7]):
         print("%-18s %6.2f%%" % (n, 100.0 * arr[i] / max(tot, 1)))
-    items = g.xRes * g.yRes   # one wave item per pixel at 64 spp
+    items = g.xRes * g.yRes * (4 if cfg == "c4" else 1)   # one wave item per 64 samples
     print("per wave item: DFS steps %.2f  wave-level prim tests %.2f  light iterations %.2f  node visits %.1f"
           % (arr[7] / items, arr[8] / items, arr[9] / items, st.wave_node_visits / items))
     names = {1: "sphere", 2: "cylinder", 3: "triangle", 4: "rectangle", 5: "prism", 6: "checker", 7: "checkerhole",
