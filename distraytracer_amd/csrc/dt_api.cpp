@@ -254,7 +254,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
     dt_scene_destroy(s);
     return rc;
   }
-  if (hipMalloc((void**)&s->d_stats, sizeof(unsigned long long) * (ST_N + 40)) != hipSuccess ||
+  if (hipMalloc((void**)&s->d_stats, sizeof(unsigned long long) * (ST_N + 48)) != hipSuccess ||
       hipMalloc(&s->d_launch, dt_launch_size()) != hipSuccess || hipEventCreate(&s->ev0) != hipSuccess ||
       hipEventCreate(&s->ev1) != hipSuccess || hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void**)&s->h_launch, dt_launch_size(), hipHostMallocDefault) != hipSuccess ||
@@ -402,7 +402,7 @@ static int enqueue_render(dt_scene* sc, const dtd::DParams& P, const std::vector
   HIPCHK(hipMemcpyAsync(sc->d_launch, sc->h_launch, dt_launch_size(), hipMemcpyHostToDevice, st));
   HIPCHK(hipEventRecord(sc->ev_copy, st));
   sc->copy_pending = true;
-  HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 40), st));
+  HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 48), st));
   static int resident = 0;
   if (!resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
   int64_t grid = P.n_items < resident ? P.n_items : resident;
@@ -667,8 +667,8 @@ int dt_write_png(const char* filename, int32_t xRes, int32_t yRes, const float* 
 
 extern "C" int dt_debug_counters(const dt_scene* sc, uint64_t* out, int32_t n)
 {
-  if (!sc || !out || n < 0 || n > 39) return fail(DT_E_INVALID, "bad arguments");
-  unsigned long long h[ST_N + 40];
+  if (!sc || !out || n < 0 || n > 47) return fail(DT_E_INVALID, "bad arguments");
+  unsigned long long h[ST_N + 48];
   HIPCHK(hipMemcpy(h, sc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
   for (int i = 0; i < n; ++i) out[i] = h[ST_N + 1 + i];
   return DT_OK;

@@ -306,7 +306,7 @@ __device__ V3 cloud_color_lane(const DParams& P, const float* __restrict__ zs, V
 // cloudColor for one (wave-uniform) ray computed by all 64 lanes: the march steps are
 // spread over lanes (the noise is 99% of the work), the per-channel recurrence then runs
 // on lanes 0..2 in step order, so every addition happens in the reference's order.
-__device__ V3 cloud_color_coop(const DParams& P, const float* __restrict__ zs, V3 ray,
+__device__ __forceinline__ V3 cloud_color_coop(const DParams& P, const float* __restrict__ zs, V3 ray,
                                float* __restrict__ dens, double* __restrict__ chan)
 {
   // the march in chunks of DT_CLOUD_CHUNK steps: densities in parallel over the lanes, then
@@ -373,7 +373,7 @@ struct Rng {
     uint32_t o[4];
     // opaque key: the 10-round key schedule is recomputed per draw (20 SALU adds) instead of
     // being hoisted into 20 SGPRs that stay live across the whole kernel and spill
-    uint32_t a = k0, b = k1;
+    uint32_t a = __builtin_amdgcn_readfirstlane(k0), b = __builtin_amdgcn_readfirstlane(k1);   // uniform key
     asm volatile("" : "+s"(a), "+s"(b));
     philox(pixel, sample, node, (purpose << 24) | sub, a, b, o);
     u0 = u01(o[0], o[1]);
@@ -1211,7 +1211,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
 #endif
   // Shadow grid: the first active lane's cell serves every lane within sg_reach cells of it.
   // Waves whose lanes all lie within that reach (coherent primary bounces) test the cell's
-  // candidate list; scattered waves (a second union list measured no better) walk the tree.
+  // candidate list; scattered waves walk the tree. Measured no better for scattered waves: a
+  // second union list; per-lane lists (each lane its own cell's list, vector loads and a
+  // per-lane shape switch: C3 1725 vs 1932, C4 843 vs 936 Mpixel-samples/s).
   if (li < P.sg_n && P.sg_base[li] >= 0) {
     const unsigned long long am = __ballot(active);
     if (!am) return false;
@@ -1266,7 +1268,7 @@ struct Counters {
   uint32_t box, prim;
   uint32_t wnodes;                   // wave-level
 #ifdef DT_STAMPS
-  unsigned long long ph[40];   // diagnostic build only: cycles per phase, event counts (wave-uniform)
+  unsigned long long ph[47];   // diagnostic build only: cycles per phase, event counts (wave-uniform)
 #endif
 };
 
@@ -1307,27 +1309,12 @@ __device__ __forceinline__ V3 rect_sample(V3 A, V3 B, V3 D, double u0, double u1
   return rect_sample_f(A, B, D, (float)u0, (float)u1);
 }
 
-// light sampleRay (geometry.cpp:2751-2849)
-// xy: the area-light sample's float pair (rect_sample's (float)U draws). cache_mode 1 stores the
-// drawn pair there, 2 reuses the stored pair instead of drawing it again (same values).
-__device__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L, int li, V3 point, uint32_t node,
-                           unsigned long long* st_sphl, float* xy = nullptr, int cache_mode = 0)
+// sphereLight::sampleRay (geometry.cpp:2770-2826, Q11: returns the sampled point) -- rejection
+// sampling with acos/sin/cos (no C2-C5 scene has a sphere light). Everything stays inlined: a real
+// call anywhere in the trace kernel costs ~25% (calling-convention register saves/spills)
+__device__ __forceinline__ V3 sphere_light_sample(const Ctx& c, const DT_CAS DLight& L, int li, V3 point,
+                                                            uint32_t node, unsigned long long* st_sphl)
 {
-  if (L.type == DT_LIGHT_POINT) return sub(v3a(L.center), point);
-  if (L.type == DT_LIGHT_RECT) {
-    float x, y;
-    if (cache_mode == 2) {
-      x = xy[0];
-      y = xy[DT_WAVE];
-    } else {
-      double u0, u1;
-      c.rng.draw(node, P_LIGHT, (uint32_t)li, u0, u1);
-      x = (float)u0;
-      y = (float)u1;
-      if (cache_mode == 1) { xy[0] = x; xy[DT_WAVE] = y; }
-    }
-    return sub(rect_sample_f(v3a(L.A), v3a(L.B), v3a(L.D), x, y), point);
-  }
   V3 C = v3a(L.center), baxis = v3a(L.baxis);
   int attempt = 0;
   double u0, u1;
@@ -1352,6 +1339,30 @@ __device__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L, int li, V3 poin
     sample_limit--;
   }
   return tmp;
+}
+
+// light sampleRay (geometry.cpp:2751-2849)
+// xy: the area-light sample's float pair (rect_sample's (float)U draws). cache_mode 1 stores the
+// drawn pair there, 2 reuses the stored pair instead of drawing it again (same values).
+__device__ __forceinline__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L, int li, V3 point, uint32_t node,
+                                           unsigned long long* st_sphl, float* xy = nullptr, int cache_mode = 0)
+{
+  if (L.type == DT_LIGHT_POINT) return sub(v3a(L.center), point);
+  if (L.type == DT_LIGHT_RECT) {
+    float x, y;
+    if (cache_mode == 2) {
+      x = xy[0];
+      y = xy[DT_WAVE];
+    } else {
+      double u0, u1;
+      c.rng.draw(node, P_LIGHT, (uint32_t)li, u0, u1);
+      x = (float)u0;
+      y = (float)u1;
+      if (cache_mode == 1) { xy[0] = x; xy[DT_WAVE] = y; }
+    }
+    return sub(rect_sample_f(v3a(L.A), v3a(L.B), v3a(L.D), x, y), point);
+  }
+  return sphere_light_sample(c, L, li, point, node, st_sphl);
 }
 
 // helpers.h:313-317 (Q10)
@@ -1793,7 +1804,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   Counters cnt;
   cnt.rays = 0; cnt.shadow = 0; cnt.tex = 0; cnt.box = 0; cnt.prim = 0; cnt.wnodes = 0;
 #ifdef DT_STAMPS
-  for (int k = 0; k < 40; ++k) cnt.ph[k] = 0;
+  for (int k = 0; k < 47; ++k) cnt.ph[k] = 0;
 #endif
 
   while (true) {
@@ -1932,7 +1943,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       atomicAdd(S.stats + ST_PRIM, pr);
       atomicAdd(S.stats + ST_WNODES, (unsigned long long)cnt.wnodes);
 #ifdef DT_STAMPS
-      for (int k = 0; k < 39; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);
+      for (int k = 0; k < 47; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);
 #endif
       if (sky_px) atomicAdd(S.stats + ST_SKY, sky_px);
       atomicAdd(S.stats + ST_RAYS, r);

@@ -22,8 +22,8 @@ def main():
     s = dt.Scene(b, g)
     out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
     st = dt.render(s, g, 240, out)
-    arr = (ctypes.c_uint64 * 39)()
-    dt.check(dt.lib.dt_debug_counters(s.handle, arr, 39))
+    arr = (ctypes.c_uint64 * 47)()
+    dt.check(dt.lib.dt_debug_counters(s.handle, arr, 47))
     tot = arr[5] + arr[6]
     print("kernel ms %.2f" % st.kernel_ms)
     for i, n in enumerate(NAMES[:7]):
@@ -40,6 +40,7 @@ def main():
           % (100.0 * arr[32] / max(tot, 1), 100.0 * arr[33] / max(tot, 1)))
     print("shadow grid per item: list tests %.1f, list walks %.2f, cell lookups inside %.2f / outside %.2f, "
           "list too long %.2f" % (arr[34] / items, arr[35] / items, arr[36] / items, arr[38] / items, arr[37] / items))
+    print("per-lane list rounds per item %.2f" % (arr[39] / items))
     print("shadow walks per item: all occluded %.2f (%.1f visits/walk), none occluded %.2f (%.1f/walk), total %.2f"
           % (arr[29] / items, arr[28] / max(arr[29], 1), arr[31] / items, arr[30] / max(arr[31], 1), arr[9] / items))
 
