@@ -157,6 +157,9 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const std::vecto
     for (auto& v : lists) v.clear();
     for (int leaf : leaves) {
       const dtd::DNodeDev& nd = nodes[leaf];
+      // the light's own shape is skipped by the shadow test (cpp:832): a leaf holding only it
+      // never occludes this light
+      if ((nd.meta & dtd::DN_SINGLE) && nd.first == L.shape_index) continue;
       int r0[3], r1[3];
       for (int a = 0; a < 3; ++a) cell_range(lo[a], hh[a], g.dim[a], m1, llo[a], lhi[a], nd.lb[a], nd.ub[a], r0[a], r1[a]);
       for (int z = r0[2]; z <= r1[2]; ++z)
