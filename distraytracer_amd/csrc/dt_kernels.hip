@@ -61,6 +61,9 @@ using namespace dtd;
 #ifndef DT_TCULL_HOIST
 #define DT_TCULL_HOIST 1
 #endif
+#ifndef DT_FIN_PARTIAL
+#define DT_FIN_PARTIAL 1   // FINISH entries write/read only their colour and depth
+#endif
 #ifndef DT_LS_CACHE
 #define DT_LS_CACHE 4   // lights whose area-sample pair is kept in LDS between the two light passes
 #endif
@@ -566,9 +569,9 @@ __device__ bool segment_hit(V3 A, V3 B, V3 ray, V3 origin)
 
 // GeoPrimitive::intersect. t only written when the reference writes it (Q16).
 __device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, GP g,
-                          V3 ray, V3 start, float shift, float& t, int& inside, V3& ccol, int& has_ccol, int& edge)
+                          V3 ray, V3 start, float shift, float& t, int& inside, int& ccol, int& edge)
 {
-  has_ccol = 0;
+  ccol = -1;
   switch (type) {
     case DT_SHAPE_SPHERE:
       return sphere_hit(g, ray, start, t, inside);
@@ -617,8 +620,8 @@ __device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, GP
         // edge-on: returns true without t; colour keeps its construction value
         if (segment_hit(A, B, ray, start) || segment_hit(A, D, ray, start) ||
             segment_hit(B, C, ray, start) || segment_hit(C, D, ray, start)) {
-          ccol = G3(g, CK_COL);
-          has_ccol = 1;
+          ccol = CK_COL;
+
           edge = 1;   // t is the stale value of the previous test: order dependent
           return true;
         }
@@ -633,17 +636,18 @@ __device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, GP
       t = tt;
       float Sq = (float)g[CK_S];
       int i = (int)(ch1 / Sq), j = (int)(ch2 / Sq);
-      V3 col = G3(g, CK_COL);
+      // the checker colour the reference stores in the shape (geometry.cpp:2314-2337), as the
+      // geom offset of that colour: the walk carries one int instead of three doubles
+      int col = CK_COL;
       if (i % 2 == 0) {
-        if (j % 2 == 0) col = G3(g, CK_COL1);
-        if (j % 2 == 1) col = G3(g, CK_COL2);
+        if (j % 2 == 0) col = CK_COL1;
+        if (j % 2 == 1) col = CK_COL2;
       }
       if (i % 2 == 1) {
-        if (j % 2 == 0) col = G3(g, CK_COL2);
-        if (j % 2 == 1) col = G3(g, CK_COL1);
+        if (j % 2 == 0) col = CK_COL2;
+        if (j % 2 == 1) col = CK_COL1;
       }
       ccol = col;
-      has_ccol = 1;
       return true;
     }
   }
@@ -992,8 +996,7 @@ struct HitRec {
   int rank;       // leaf rank of the hit in the reference's gather order (fast-tree ties)
   int edge;       // a checkerboard edge-on hit (Q16) was taken
   int inside;
-  int has_ccol;
-  V3 ccol;
+  int ccol;       // checker colour of the hit (geom offset), -1: the material colour
 };
 
 // closest hit over the lanes with `active` (cpp:491-538)
@@ -1013,7 +1016,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
   h.rank = 0x7fffffff;
   h.edge = 0;
   h.inside = 0;
-  h.has_ccol = 0;
+  h.ccol = -1;
   int i = 0;
   const int n_nodes = ftree ? P.n_fnodes : P.n_nodes;
   while (i < n_nodes) {
@@ -1040,9 +1043,8 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
           DT_CNT(10 + (type & 7));   // closest-hit prim tests by type (8 -> 10)
           if (hb) {
             DT_WORK(cnt.prim++);
-            int ins = 0, hc = 0;
-            V3 cc;
-            if (shape_hit(S, sid, type, flags, cas(S.geom) + off, ray, org, shift, t_dist, ins, cc, hc, h.edge)) {
+            int ins = 0, cc = -1;
+            if (shape_hit(S, sid, type, flags, cas(S.geom) + off, ray, org, shift, t_dist, ins, cc, h.edge)) {
               any = true;
               // strict < in the reference's gather order; the fast tree visits leaves in another
               // order, so equal distances go to the lower reference rank
@@ -1055,8 +1057,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
 #if DT_TCULL_HOIST
                 tcull = t_dist == FLT_MAX ? FLT_MAX : t_dist * 1.0001f + 1e-4f;
 #endif
-                h.has_ccol = hc;
-                if (hc) h.ccol = cc;
+                h.ccol = cc;
               }
             }
           }
@@ -1392,6 +1393,21 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     bool have = false;
     Entry e;
     while (sp > 0) {
+#if DT_FIN_PARTIAL
+      // read the depth word first: a FINISH entry only carries its colour
+      const int d = stack[--sp].depth;
+      if (d < 0) {
+        const V3 a = stack[sp].a;
+        const int l = threadIdx.x & (DT_WAVE - 1);   // out.color += own light (in LDS)
+        ocol[0][l] = ocol[0][l] + a.x;
+        ocol[1][l] = ocol[1][l] + a.y;
+        ocol[2][l] = ocol[2][l] + a.z;
+      } else if (d > 0) {
+        e = stack[sp];
+        have = true;
+        break;
+      }
+#else
       e = stack[--sp];
       if (e.depth < 0) {
         const int l = threadIdx.x & (DT_WAVE - 1);   // out.color += own light (in LDS)
@@ -1402,6 +1418,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
         have = true;
         break;
       }
+#endif
     }
     if (!__ballot(have)) break;
     DT_CNT(7);
@@ -1436,7 +1453,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       isectP = add(eye, mul(h.t_min, ray));
       normal = shape_norm(hd.type, hd.flags, g, isectP, shift, S.stats + ST_PRISM);
       in = normalized(ray);
-      shape_color = h.has_ccol ? h.ccol : v3a(M.color);
+      shape_color = h.ccol >= 0 ? G3(g, h.ccol) : v3a(M.color);
       out.in_motion = (M.flags & DT_F_MOTION) != 0;
       if (dot(mul(1e4, in), normal) >= 0) normal = mul(-1, normal);   // fixNorm
 
@@ -1704,9 +1721,14 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     DT_T(t6);
     DT_ACC(4, t3, t6);
     if (fin_slot >= 0) {
+#if DT_FIN_PARTIAL
+      stack[fin_slot].a = own;
+      stack[fin_slot].depth = -1;
+#else
       Entry f;
       f.a = own; f.b = v3(0, 0, 0); f.k = 0; f.depth = -1; f.key = 0; f._pad = 0;
       stack[fin_slot] = f;
+#endif
     }
   }
 }
