@@ -1367,9 +1367,9 @@ __device__ __forceinline__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L,
 }
 
 // helpers.h:313-317 (Q10)
-__device__ __forceinline__ float schlick_complex(float cos_theta, double r0, double r1)
+// R0 = (float)(((r0-1)^2 + r1^2) / ((r0+1)^2 + r1^2)) is per material (DMat::ct_r0, host)
+__device__ __forceinline__ float schlick_complex(float cos_theta, float R0)
 {
-  float R0 = (float)((pw2(r0 - 1) + pw2(r1)) / (pw2(r0 + 1) + pw2(r1)));
   return (float)((R0 + (1 - R0)) + pw5((double)(1 - cos_theta)));
 }
 
@@ -1668,8 +1668,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           } else
 #endif
           if (M.model == DT_MODEL_OREN_NAYAR) {
-            float A = (float)(1.0 - (0.5 * pw2((double)roughness)) / (pw2((double)roughness) + 0.33));
-            float B = (float)((0.45 * pw2((double)roughness)) / (pw2((double)roughness) + 0.09));
+            const float A = M.on_a, B = M.on_b;   // per material (host, cpp:896-897)
             float vn = (float)dot(e_dir, normal);
             float ln = (float)dot(sn, normal);
             float irradiance = fmaxr(0.0f, ln);
@@ -1696,7 +1695,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
             float G = 1.0f;
             if (G1 < G) G = G1;
             if (G2 < G) G = G2;
-            float F = schlick_complex(vn, M.refr[0], M.refr[1]);
+            float F = schlick_complex(vn, M.ct_r0);
             float fdg = F * D * G;
             double den = (double)(ln * vn) * M_PI;
             V3 shader_rgb = add(mul(fmaxr(0.0f, ln), mul(0.4, lc)), divs(mul(fdg, mul(0.8, lc)), den));

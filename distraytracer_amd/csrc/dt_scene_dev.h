@@ -55,6 +55,10 @@ struct alignas(16) DMat {
   int32_t tex_w, tex_h, tex_ch;
   int64_t tex_off; // byte offset into tex pool
   float roughness, radius;
+  // per-material constants of the BRDFs, computed on the host with the reference's expressions
+  // (same IEEE double operations, no contraction): schlick's R0 (helpers.h:313-317), Oren-Nayar's
+  // A and B (render_final_project.cpp:896-897)
+  float ct_r0, on_a, on_b, _pad_m;
   double refr[2];
   double color[3];
   double bordercolor[3];

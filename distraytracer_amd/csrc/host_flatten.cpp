@@ -229,6 +229,13 @@ int flatten_scene(const dt_scene_desc& d, const dt_globals& g, FlatScene& out, s
     m.radius = s.radius;
     m.refr[0] = s.refr[0];
     m.refr[1] = s.refr[1];
+    {
+      const double r0 = m.refr[0], r1 = m.refr[1], rr = (double)m.roughness;
+      m.ct_r0 = (float)(((r0 - 1) * (r0 - 1) + r1 * r1) / ((r0 + 1) * (r0 + 1) + r1 * r1));
+      m.on_a = (float)(1.0 - (0.5 * (rr * rr)) / ((rr * rr) + 0.33));
+      m.on_b = (float)((0.45 * (rr * rr)) / ((rr * rr) + 0.09));
+      m._pad_m = 0;
+    }
     for (int k = 0; k < 3; ++k) {
       m.color[k] = s.color[k];
       m.bordercolor[k] = s.bordercolor[k];
