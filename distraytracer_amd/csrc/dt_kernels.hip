@@ -1678,7 +1678,14 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
             float alpha = fmaxr(vn_theta, ln_theta), beta = fminr(vn_theta, ln_theta);
             float f = A + B * angleDiff * cr_sinf(alpha) * cr_tanf(beta);
             ray_col = mul(f, mul(irradiance, cwise(shape_color, lc)));
-          } else if (M.model == DT_MODEL_COOK_TORRANCE) {
+          }
+#ifdef DT_ABL_NOCT
+          else if (M.model == DT_MODEL_COOK_TORRANCE) { ray_col = cwise(shape_color, lc); }
+#endif
+#ifdef DT_ABL_NOPHONG
+          else if (M.model == DT_MODEL_PHONG) { ray_col = cwise(shape_color, lc); }
+#endif
+          else if (M.model == DT_MODEL_COOK_TORRANCE) {
             V3 H = normalized(add(e_dir, sray));
             float hn = (float)dmax(0.0, dot(normal, H));
             float vh = (float)dot(e_dir, H);
