@@ -187,6 +187,8 @@ def main():
         achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
         peak = 8000.0
         pmc = load_pmc_traffic() or {}
+        if pmc.get("config", "c3") != args.config:
+            pmc = {}   # the committed PMC profile is of another workload
         traffic = pmc.get("hbm_bytes_per_launch")
         cpu = None
         e2e = end_to_end_ms(dt, args.config, dev) if world == 1 else None

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--depth", type=int, default=10)
     ap.add_argument("--out", default="", help="directory for frame.NNNN.png (none: keep on the GPU)")
+    ap.add_argument("--per-frame", action="store_true", help="print host-build and render ms per frame (stderr)")
     args = ap.parse_args()
 
     import torch
@@ -51,14 +52,23 @@ def main():
     t0 = time.perf_counter()
     samples = 0
     for n in mine:
+        f0 = time.perf_counter()
         g = dt.globals_default()   # fresh globals per frame (one process per frame in the reference)
         g.use_model = 0
         g.xRes, g.yRes, g.antialias_samples, g.max_depth = W, H, args.spp, args.depth
         built = dt.build_scene("final", n * 8, g)
         scene = dt.Scene(built, g)
+        f1 = time.perf_counter()
         img = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
         st = dt.render(scene, g, n * 8, img)
+        torch.cuda.synchronize()
+        f2 = time.perf_counter()
         samples += st.samples
+        if args.per_frame:
+            print(json.dumps({"n": n, "frame": n * 8, "host_ms": round((f1 - f0) * 1e3, 1),
+                              "render_ms": round((f2 - f1) * 1e3, 1), "spp": st.samples // max(st.pixels, 1),
+                              "rays_per_sample": round(st.rays / max(st.samples, 1), 3),
+                              "sky_pixels": getattr(st, "sky_pixels", None)}), file=sys.stderr, flush=True)
         if args.out:
             os.makedirs(args.out, exist_ok=True)
             dt.write_png(os.path.join(args.out, "frame.%04d.png" % n), g, img.cpu().numpy())
