@@ -43,6 +43,8 @@ struct HScene {
   const float* cloud_z;
   unsigned long long* stats;
   unsigned long long* queue;
+  const void* bnodes;       // motion-blur bump tree (host_fasttree.cpp)
+  const int32_t* bparent;   // parent of every reference-tree node
 };
 
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
@@ -95,6 +97,10 @@ struct dt_scene {
   void* d_nodes = nullptr;
   void* d_fnodes = nullptr;
   int n_fnodes = 0;
+  void* d_bnodes = nullptr;    // bump tree for motion-blur passes (0 nodes: they walk the reference tree)
+  void* d_bparent = nullptr;
+  int n_bnodes = 0;
+  float bump_pad = 0;          // y padding of its leaves: the largest |shift| a blur pass can draw
   ShadowGrid sg;
   void* d_sg_cells = nullptr;
   void* d_sg_list = nullptr;
@@ -225,6 +231,24 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
       for (int a = 0; a < 3; ++a)
         if (!(n.lb[a] <= n.ub[a])) s->boxes_ordered = 0;
   if (fnodes.empty()) fnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
+  // Motion-blur bump tree: leaves padded by the largest |val| of cpp:1108-1135 for these globals
+  // (|move_per_frame| d + |accel_t| d^3 over d = frame_sample - frame in [0, frame_range], plus
+  // margin for the float evaluation). The device checks every lane's shift against the pad and
+  // walks the reference tree when one exceeds it. DT_BUMP_TREE=0 disables it.
+  std::vector<dtd::DNodeDev> bnodes;
+  std::vector<int32_t> bparent = tree_parents(dnodes);
+  {
+    const char* bt = getenv("DT_BUMP_TREE");
+    const double d = fabs((double)g->frame_range) * (1.0 + 1e-3) + 1e-3;
+    const double pad = ((double)fabsf(g->move_per_frame) * d + (double)fabsf(g->accel_t) * d * d * d) * 1.01 + 1e-6;
+    s->bump_pad = (float)pad;
+    if (!(bt && bt[0] == '0') && g->blur_samples > 0 && pad > 0 && pad < 1e3 && build_fast_tree(dnodes, bnodes, pad))
+      s->n_bnodes = (int)bnodes.size();
+    else
+      bnodes.clear();
+  }
+  if (bnodes.empty()) bnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
+  if (bparent.empty()) bparent.push_back(-1);
   // shadow grid (host_shadowgrid.cpp); DT_SHADOW_GRID=0: every shadow test walks a tree
   const char* sgv = getenv("DT_SHADOW_GRID");
   const char* sgc = getenv("DT_SG_CELLS");
@@ -248,7 +272,8 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
     dt_scene_destroy(s);
     return rc;
   }
-  if ((rc = upload(dnodes, &s->d_nodes)) || (rc = upload(fnodes, &s->d_fnodes)) || (rc = upload(leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
+  if ((rc = upload(dnodes, &s->d_nodes)) || (rc = upload(fnodes, &s->d_fnodes)) || (rc = upload(bnodes, &s->d_bnodes)) ||
+      (rc = upload(bparent, &s->d_bparent)) || (rc = upload(leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
       (rc = upload(f.geom, &s->d_geom)) || (rc = upload(f.mat, &s->d_mat)) || (rc = upload(f.lights, &s->d_lights)) ||
       (rc = upload(f.tex, &s->d_tex))) {
     dt_scene_destroy(s);
@@ -269,7 +294,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
 void dt_scene_destroy(dt_scene* s)
 {
   if (!s) return;
-  void* bufs[] = {s->d_nodes, s->d_fnodes, s->d_sg_cells, s->d_sg_list, s->d_leaf, s->d_hdr, s->d_geom, s->d_mat, s->d_lights, s->d_tex, s->d_zs,
+  void* bufs[] = {s->d_nodes, s->d_fnodes, s->d_bnodes, s->d_bparent, s->d_sg_cells, s->d_sg_list, s->d_leaf, s->d_hdr, s->d_geom, s->d_mat, s->d_lights, s->d_tex, s->d_zs,
                   s->d_stats, s->d_launch};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -349,6 +374,8 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   if (g->perlin_cloud && zs.size() > 2048) return fail(DT_E_LIMIT, "clouddist/0.05 exceeds 2048 march steps");
   P.n_nodes = (int32_t)sc->flat.bvh.nodes.size();
   P.n_fnodes = sc->n_fnodes;
+  P.n_bnodes = sc->n_bnodes;
+  P.bump_pad = sc->bump_pad;
   P.ftree_mode = sc->ftree_mode;
   P.boxes_ordered = sc->boxes_ordered;
   P.sg_n = sc->sg.n_lights;
@@ -384,6 +411,8 @@ static int enqueue_render(dt_scene* sc, const dtd::DParams& P, const std::vector
   HScene hs;
   hs.nodes = sc->d_nodes;
   hs.fnodes = sc->d_fnodes;
+  hs.bnodes = sc->d_bnodes;
+  hs.bparent = (const int32_t*)sc->d_bparent;
   hs.sg_cells = (const uint32_t*)sc->d_sg_cells;
   hs.sg_list = (const int32_t*)sc->d_sg_list;
   hs.leaf_idx = (const int32_t*)sc->d_leaf;

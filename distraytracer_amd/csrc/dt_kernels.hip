@@ -107,6 +107,8 @@ struct DScene {
   const float* cloud_z;   // float z sequence of cloudColor's loop (cpp:172)
   unsigned long long* stats;
   unsigned long long* queue;
+  const DNodeDev* bnodes;   // bump tree for motion-blur passes (host_fasttree.cpp; leaf skip = reference index)
+  const int32_t* bparent;   // parent of every reference node (-1: root)
 };
 
 // pow(x, n) for the integer exponents the reference writes as pow(x, 2.0) etc. pow(x, 1) is x
@@ -999,14 +1001,45 @@ struct HitRec {
   int ccol;       // checker colour of the hit (geom offset), -1: the material colour
 };
 
+// Motion-blur passes on the bump tree: whether the reference gathers the leaf `r` (its index in
+// the reference tree) for this lane: the bumped leaf box passes (node_hit<true>) and so do all its
+// reference ancestors -- implied when the unbumped leaf box passes (the ancestors contain it and
+// the finite-ray slab test is monotone), otherwise tested up the parent chain (host_fasttree.cpp).
+__device__ __forceinline__ bool bump_leaf_gathered(const DScene& S, const Walk& w, int r, float shift, V3 st)
+{
+  const DNodeDev rn = cas(S.nodes)[r];
+  const bool bumped = box_hit(rn, rn.lb[1] - shift, rn.ub[1] + shift, w.rb, st);
+  const bool unb = box_hit(rn, rn.lb[1], rn.ub[1], w.rb, st);
+  bool ok = bumped & unb;
+  const bool need = bumped & !unb;
+  if (__ballot(need)) {
+    bool anc = true;
+    for (int a = uni(cas(S.bparent)[r]); a >= 0; a = uni(cas(S.bparent)[a])) {
+      const DNodeDev an = cas(S.nodes)[a];
+      anc = anc & box_hit(an, an.lb[1], an.ub[1], w.rb, st);
+    }
+    ok = ok | (need & anc);
+  }
+  return ok;
+}
+
+// every active lane's motion-blur shift lies within the bump tree's padding
+__device__ __forceinline__ bool bump_tree_ok(const DParams& P, bool active, float shift)
+{
+  return P.n_bnodes > 0 && !__ballot(active && !(fabsf(shift) <= P.bump_pad));
+}
+
 // closest hit over the lanes with `active` (cpp:491-538)
-template <bool GENERAL, class CNT>
+// MODE 0: finite rays, no bump (fast tree, culled); 1: the reference tree, exact for any wave;
+// 2: finite rays of a motion-blur pass on the bump tree (culled, exact gather at the leaves)
+template <int MODE, class CNT>
 __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams& P, const Walk& w, bool active, V3 ray,
                                                  V3 org, float shift, HitRec& h, CNT& cnt)
 {
+  constexpr bool GENERAL = MODE == 1, BUMP = MODE == 2;
   // fast walks use the alternative tree when one was built (DT_FAST_TREE), else the reference's
-  const bool ftree = !GENERAL && P.n_fnodes > 0 && (P.ftree_mode & 1);
-  const DNodeDev* const NODES = ftree ? S.fnodes : S.nodes;
+  const bool ftree = BUMP || (!GENERAL && P.n_fnodes > 0 && (P.ftree_mode & 1));
+  const DNodeDev* const NODES = BUMP ? S.bnodes : ftree ? S.fnodes : S.nodes;
   int resume = active ? 0 : 0x7fffffff;
   float t_dist = FLT_MAX;
   float tcull = FLT_MAX;   // culling bound from the best hit so far (updated with it)
@@ -1018,7 +1051,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
   h.inside = 0;
   h.ccol = -1;
   int i = 0;
-  const int n_nodes = ftree ? P.n_fnodes : P.n_nodes;
+  const int n_nodes = BUMP ? P.n_bnodes : ftree ? P.n_fnodes : P.n_nodes;
   while (i < n_nodes) {
     const DNodeDev nd = cas(NODES)[i];
     // fast walks need no per-lane resume point: every box contains its subtree's boxes and the
@@ -1028,10 +1061,11 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
 #if !DT_TCULL_HOIST
     tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
 #endif
-    const bool hb = act & node_hit<GENERAL>(w, nd, shift, org, tcull);
+    bool hb = act & node_hit<GENERAL>(w, nd, shift, org, tcull);
     DT_WORK(cnt.wnodes++; cnt.box += act);
     DT_CNT(26);
     if (nd.meta & DN_LEAF) {
+      if (BUMP && __ballot(hb)) hb = hb & bump_leaf_gathered(S, w, nd.skip, shift, org);
       if (__ballot(hb)) {
         DT_T(q0);
         const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
@@ -1080,12 +1114,15 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
                                             HitRec& h, CNT& cnt)
 {
   const Walk w = make_walk(P, active, ray, org, shift);
-  if (w.inf_wave || w.bump_wave) return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
-  const bool any = closest_hit_walk<false>(S, P, w, active, ray, org, shift, h, cnt);
+  if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift)))
+    return closest_hit_walk<1>(S, P, w, active, ray, org, shift, h, cnt);
+  const bool any = w.bump_wave ? closest_hit_walk<2>(S, P, w, active, ray, org, shift, h, cnt)
+                               : closest_hit_walk<0>(S, P, w, active, ray, org, shift, h, cnt);
   // an edge-on checkerboard hit keeps the previous test's t (Q16): only the reference order
-  // reproduces it, so with the alternative tree such waves (never seen in practice) repeat the
+  // reproduces it, so with the alternative trees such waves (never seen in practice) repeat the
   // walk on the reference tree
-  if (P.n_fnodes > 0 && (P.ftree_mode & 1) && __ballot(h.edge)) return closest_hit_walk<true>(S, P, w, active, ray, org, shift, h, cnt);
+  if ((w.bump_wave || (P.n_fnodes > 0 && (P.ftree_mode & 1))) && __ballot(h.edge))
+    return closest_hit_walk<1>(S, P, w, active, ray, org, shift, h, cnt);
   return any;
 }
 
@@ -1123,13 +1160,14 @@ __device__ __forceinline__ float shadow_tcull(float t_max)
 
 // any-hit shadow test (cpp:806-855): box test with sray from isectP+sray*1e-3, shape test
 // with normalized sray from isectP+sn*1e-3, skipping the light's own shape.
-template <bool GENERAL, class CNT>
+template <int MODE, class CNT>
 __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P, const Walk& w, bool active, V3 bstart,
                                               V3 sn, V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
 {
+  constexpr bool GENERAL = MODE == 1, BUMP = MODE == 2;   // as closest_hit_walk
   // fast walks use the alternative tree when one was built (DT_FAST_TREE), else the reference's
-  const bool ftree = !GENERAL && P.n_fnodes > 0 && (P.ftree_mode & 2);
-  const DNodeDev* const NODES = ftree ? S.fnodes : S.nodes;   // any-hit: order free
+  const bool ftree = !BUMP && !GENERAL && P.n_fnodes > 0 && (P.ftree_mode & 2);
+  const DNodeDev* const NODES = BUMP ? S.bnodes : ftree ? S.fnodes : S.nodes;   // any-hit: order free
   int resume = active ? 0 : 0x7fffffff;
   bool occl = false;
   const float tcull = shadow_tcull(t_max);
@@ -1140,17 +1178,18 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
 #ifdef DT_STAMPS
   unsigned long long nv = 0;
 #endif
-  const int n_nodes = ftree ? P.n_fnodes : P.n_nodes;
+  const int n_nodes = BUMP ? P.n_bnodes : ftree ? P.n_fnodes : P.n_nodes;
   while (i < n_nodes) {
     const DNodeDev nd = cas(NODES)[i];
     const bool act = GENERAL ? resume <= i : active & !occl;   // see closest_hit_walk
-    const bool hb = act & node_hit<GENERAL>(w, nd, shift, bstart, tcull);
+    bool hb = act & node_hit<GENERAL>(w, nd, shift, bstart, tcull);
     DT_WORK(cnt.wnodes++; cnt.box += act);
     DT_CNT(27);
 #ifdef DT_STAMPS
     ++nv;
 #endif
     if (nd.meta & DN_LEAF) {
+      if (BUMP && __ballot(hb)) hb = hb & bump_leaf_gathered(S, w, nd.skip, shift, bstart);
       if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, shift, cnt);
       if (GENERAL) {
         if (act) resume = occl ? 0x7fffffff : nd.skip;
@@ -1205,8 +1244,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
                                          V3 sstart, float t_max, int skip_shape, int li, float shift, CNT& cnt)
 {
   const Walk w = make_walk(P, active, sray, bstart, shift);
-  if (w.inf_wave || w.bump_wave)
-    return occluded_walk<true>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+  if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift)))
+    return occluded_walk<1>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+  if (w.bump_wave) return occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 #ifdef DT_ABL_NOSHADOW
   return false;
 #endif
@@ -1241,7 +1281,7 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       DT_CNT(37);
     }
   }
-  return occluded_walk<false>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+  return occluded_walk<0>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 }
 
 // =====================================================================================

@@ -112,6 +112,8 @@ struct DParams {
   int32_t reflect, nogloss, perlin_cloud;
   int32_t n_nodes, n_lights, n_shapes;
   int32_t n_fnodes;       // fast tree (host_fasttree.cpp); 0: every wave walks the reference tree
+  int32_t n_bnodes;       // motion-blur bump tree (host_fasttree.cpp); 0: blur passes walk the reference tree
+  float bump_pad;         // its leaves' y padding; lanes with |shift| > bump_pad walk the reference tree
   int32_t sg_n;           // shadow grid: lights 0..sg_n-1 (sg_base < 0: none for that light)
   int32_t sg_dim[3];
   int32_t sg_base[DT_MAX_SGRID];

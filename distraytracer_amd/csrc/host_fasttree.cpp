@@ -11,8 +11,18 @@
 // SAH over the leaf boxes, each inner box the exact union of its leaves), so it gathers the same
 // leaves with fewer visits. Order only matters for the closest-hit tie rule (strict <, first in
 // the reference's gather order): every leaf carries its rank in that order and the device breaks
-// equal-t ties by rank. Not monotone, hence never used: motion-blur leaf bumps (Q19, interior
-// boxes unbumped) and axis-parallel rays (isinf branch); those waves walk the reference tree.
+// equal-t ties by rank. Axis-parallel rays (isinf branch) are not monotone: those waves walk the
+// reference tree.
+//
+// Motion-blur passes (bumpBVH, helpers.h:530-552) pad every LEAF box by the sample's shift in y
+// and leave the inner boxes alone, so the gathered set there is {leaves whose bumped box passes
+// and whose reference ancestors all pass}. The bump tree (ypad > 0) holds the same leaves with
+// their y-bounds padded by the largest |shift| the frame can draw, under SAH inner nodes: every
+// bumped leaf box and every shifted "rectangle" lies inside its padded leaf box, so a wave-uniform
+// walk over it reaches every leaf the reference could gather. At such a leaf the device decides
+// the reference's predicate exactly: the bumped box test, and the ancestors -- implied when the
+// unbumped leaf box passes (containment + monotonicity, as above), tested one by one up the
+// reference tree (tree_parents) otherwise. Leaves keep their reference index in `skip`.
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -37,10 +47,11 @@ double area(const double lb[3], const double ub[3])
 
 struct Builder {
   const std::vector<dtd::DNodeDev>& ref;   // reference tree, device format
+  double ypad;                             // bump tree: leaf boxes padded by this in y
   std::vector<LeafRef> leaves;
   std::vector<dtd::DNodeDev> out;
 
-  explicit Builder(const std::vector<dtd::DNodeDev>& r) : ref(r) {}
+  Builder(const std::vector<dtd::DNodeDev>& r, double yp) : ref(r), ypad(yp) {}
 
   void box_of(const std::vector<int>& ids, int lo, int hi, double lb[3], double ub[3]) const
   {
@@ -61,6 +72,10 @@ struct Builder {
       dtd::DNodeDev nd = ref[L.node];
       nd.meta = (nd.meta & 0xffffu) | ((uint32_t)L.rank << 16);
       nd.skip = me + 1;
+      if (ypad > 0) {   // bump tree: padded box, skip = the leaf's index in the reference tree
+        for (int a = 0; a < 3; ++a) { nd.lb[a] = L.lb[a]; nd.ub[a] = L.ub[a]; }
+        nd.skip = L.node;
+      }
       out[me] = nd;
       return me;
     }
@@ -116,10 +131,10 @@ struct Builder {
 
 // ref: the reference tree in device format (pre-order, last child first, skip links).
 // Returns false (and leaves `out` empty) when the tree cannot carry 16-bit leaf ranks.
-bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNodeDev>& out)
+bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNodeDev>& out, double ypad)
 {
   out.clear();
-  Builder b(ref);
+  Builder b(ref, ypad);
   for (size_t i = 0; i < ref.size(); ++i) {
     if (!(ref[i].meta & dtd::DN_LEAF)) continue;
     LeafRef L;
@@ -127,6 +142,11 @@ bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNo
       L.lb[a] = ref[i].lb[a];
       L.ub[a] = ref[i].ub[a];
       L.c[a] = 0.5 * (L.lb[a] + L.ub[a]);
+    }
+    if (ypad > 0) {
+      L.lb[1] = L.lb[1] - ypad;
+      L.ub[1] = L.ub[1] + ypad;
+      if (!(L.lb[1] <= L.ub[1])) return false;
     }
     L.node = (int)i;
     L.rank = (int)b.leaves.size();
@@ -138,6 +158,19 @@ bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNo
   b.build(ids, 0, (int)ids.size());
   out.swap(b.out);
   return true;
+}
+
+std::vector<int32_t> tree_parents(const std::vector<dtd::DNodeDev>& ref)
+{
+  // pre-order with skip = end of the subtree for inner nodes (a leaf's subtree ends at i + 1)
+  std::vector<int32_t> parent(ref.size(), -1);
+  std::vector<int> open;
+  for (int i = 0; i < (int)ref.size(); ++i) {
+    while (!open.empty() && ref[open.back()].skip <= i) open.pop_back();
+    parent[i] = open.empty() ? -1 : open.back();
+    if (!(ref[i].meta & dtd::DN_LEAF)) open.push_back(i);
+  }
+  return parent;
 }
 
 }  // namespace dth

@@ -14,21 +14,25 @@ NAMES = ["pop", "closest_hit", "hit+children", "occluded", "light loop rest", "s
 
 def main():
     # config: c3 (default) or c4 (use_model, 256 spp)
+    # optional: frame (buildFinal(frame), C5 frames: depth 10 as tools/animate.py) and WxH
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    frame = int(sys.argv[2]) if len(sys.argv) > 2 else 240
+    W, H = (int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "1920x1080").split("x"))
     g = dt.globals_default()
     g.use_model = 1 if cfg == "c4" else 0
-    b = dt.build_scene("final", 240, g)
-    g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.brdf_samples = 1920, 1080, 256 if cfg == "c4" else 64, 8, 2
+    b = dt.build_scene("final", frame, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.brdf_samples = W, H, 256 if cfg == "c4" else 64, \
+        8 if frame == 240 else 10, 2
     s = dt.Scene(b, g)
     out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
-    st = dt.render(s, g, 240, out)
+    st = dt.render(s, g, frame, out)
     arr = (ctypes.c_uint64 * 47)()
     dt.check(dt.lib.dt_debug_counters(s.handle, arr, 47))
     tot = arr[5] + arr[6]
     print("kernel ms %.2f" % st.kernel_ms)
     for i, n in enumerate(NAMES[:7]):
         print("%-18s %6.2f%%" % (n, 100.0 * arr[i] / max(tot, 1)))
-    items = g.xRes * g.yRes * (4 if cfg == "c4" else 1)   # one wave item per 64 samples
+    items = st.pixels * (4 if cfg == "c4" else 1)   # one wave item per 64 samples
     print("per wave item: DFS steps %.2f  wave-level prim tests %.2f  light iterations %.2f  node visits %.1f"
           % (arr[7] / items, arr[8] / items, arr[9] / items, st.wave_node_visits / items))
     names = {1: "sphere", 2: "cylinder", 3: "triangle", 4: "rectangle", 5: "prism", 6: "checker", 7: "checkerhole",
