@@ -254,7 +254,8 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
   const char* sgc = getenv("DT_SG_CELLS");
   const char* sgr = getenv("DT_SG_REACH");
   if ((sgv && sgv[0] == '0') ||
-      !build_shadow_grid(dnodes, f.lights, s->sg, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : 0.5f))
+      !build_shadow_grid(dnodes, f, s->sg, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : 0.5f,
+                         s->n_bnodes > 0 ? (double)s->bump_pad : 0.0))
     s->sg = ShadowGrid();
   if (getenv("DT_SG_VERBOSE")) {
     size_t cells = s->sg.cells.size() / 2, tree = 0, sum = 0, mx = 0;
@@ -264,9 +265,10 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
       sum += n;
       mx = std::max(mx, (size_t)n);
     }
-    fprintf(stderr, "shadow grid: lights %d dim %dx%dx%d cells %zu (tree %zu) mean list %.2f max %zu list pool %zu\n",
+    fprintf(stderr, "shadow grid: lights %d dim %dx%dx%d cells %zu (tree %zu) mean list %.2f max %zu list pool %zu "
+            "plane-culled %ld ypad %g\n",
             s->sg.n_lights, s->sg.dim[0], s->sg.dim[1], s->sg.dim[2], cells, tree,
-            cells > tree ? (double)sum / (cells - tree) : 0.0, mx, s->sg.list.size());
+            cells > tree ? (double)sum / (cells - tree) : 0.0, mx, s->sg.list.size(), s->sg.plane_dropped, s->sg.ypad);
   }
   if ((rc = upload(s->sg.cells, &s->d_sg_cells)) || (rc = upload(s->sg.list, &s->d_sg_list))) {
     dt_scene_destroy(s);
@@ -386,6 +388,7 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   }
   for (int l = 0; l < DT_MAX_SGRID; ++l) P.sg_base[l] = sc->sg.base[l];
   P.sg_reach = sc->sg.reach;
+  P.sg_ypad = (float)sc->sg.ypad;
 
   P.n_lights = (int32_t)sc->flat.lights.size();
   P.n_shapes = (int32_t)sc->flat.hdr.size();

@@ -1215,17 +1215,20 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
 
 // The shadow test over a cell's candidate list (host_shadowgrid.cpp): the same box test and
 // shape tests as the walk, on the only leaves that can hold an occluder for this cell and light.
-template <class CNT>
+// BUMP: a motion-blur pass (lists built with sg_ypad >= bump_pad): the exact bumped gather test
+template <bool BUMP, class CNT>
 __device__ bool occluded_list(const DScene& S, const Walk& w, bool active, V3 bstart, V3 sn, V3 sstart, float t_max,
-                              int skip_shape, uint32_t off, uint32_t n, CNT& cnt)
+                              int skip_shape, float shift, uint32_t off, uint32_t n, CNT& cnt)
 {
   bool occl = false;
   const float tcull = shadow_tcull(t_max);
   for (uint32_t k = 0; k < n; ++k) {
-    const DNodeDev nd = cas(S.nodes)[cas(S.sg_list)[off + k]];
-    const bool hb = active & !occl & node_hit<false>(w, nd, 0.0f, bstart, tcull);
+    const int r = uni(cas(S.sg_list)[off + k]);
+    const DNodeDev nd = cas(S.nodes)[r];
+    const bool hb = active & !occl &
+                    (BUMP ? bump_leaf_gathered(S, w, r, shift, bstart) : node_hit<false>(w, nd, 0.0f, bstart, tcull));
     DT_CNT(34);
-    if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, 0.0f, cnt);
+    if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, shift, cnt);
     if (!__ballot(active & !occl)) break;
   }
   return occl;
@@ -1246,7 +1249,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   const Walk w = make_walk(P, active, sray, bstart, shift);
   if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift)))
     return occluded_walk<1>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
-  if (w.bump_wave) return occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+  // blur passes use the grid when its lists were built for their shifts (sg_ypad)
+  const bool bump_list = w.bump_wave && P.sg_ypad >= P.bump_pad;
+  if (w.bump_wave && !bump_list) return occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 #ifdef DT_ABL_NOSHADOW
   return false;
 #endif
@@ -1276,11 +1281,13 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       const uint32_t off = e[0], n = e[1];
       if (n != 0xffffffffu) {
         DT_CNT(35);
-        return occluded_list(S, w, active, bstart, sn, sstart, t_max, skip_shape, off, n, cnt);
+        return bump_list ? occluded_list<true>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, off, n, cnt)
+                         : occluded_list<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, off, n, cnt);
       }
       DT_CNT(37);
     }
   }
+  if (w.bump_wave) return occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
   return occluded_walk<0>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 }
 

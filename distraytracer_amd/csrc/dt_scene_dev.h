@@ -119,6 +119,7 @@ struct DParams {
   int32_t sg_base[DT_MAX_SGRID];
   float sg_lo[3], sg_inv[3];
   float sg_reach;         // a cell's list also covers points this many cells outside it
+  float sg_ypad;          // the lists also hold for blur passes whose |shift| <= sg_ypad
   int32_t ftree_mode;     // walks that use it: bit 0 closest hit, bit 1 shadow
   int32_t boxes_ordered;  // every node of both trees has lb <= ub (finite walks take slab ends by min/max)
   int32_t n_cloud_steps;

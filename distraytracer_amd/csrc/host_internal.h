@@ -33,9 +33,12 @@ struct ShadowGrid {
   float reach = 0.5f;                // a cell's list covers points this many cells outside it
   std::vector<uint32_t> cells;       // (offset into list, count | 0xffffffff: walk the tree) per cell
   std::vector<int32_t> list;         // leaf node indices (reference tree)
+  double ypad = 0;                   // lists also hold for blur passes with |shift| <= ypad
+  long plane_dropped = 0;            // (leaf, cell) pairs left out by plane culling (diagnostic)
 };
-bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const std::vector<dtd::DLight>& lights,
-                       ShadowGrid& g, double target_cells = 32768, float reach = 0.5f);
+struct FlatScene;
+bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene& fs, ShadowGrid& g,
+                       double target_cells = 32768, float reach = 0.5f, double ypad = 0);
 
 // device-layout scene produced from a descriptor (host_flatten.cpp)
 struct FlatScene {

@@ -12,7 +12,21 @@
 // the leaves whose box meets the hull. The device tests exactly those leaves (box test, then the
 // shapes), which answers as the full gather does. Sphere lights are excluded: their sampleRay
 // returns the sampled point itself (Q11), so the "segment" does not end on the light.
+//
+// Plane culling: a leaf whose box meets the swept box is still left out when every one of its
+// shapes is separated from the segments by a plane: all of the widened cell box and the light box
+// lie strictly on one side of a rectangle's, checkerboard's or triangle's plane, or on the
+// outside of one face plane of a (convex) RectPrismV2. Such a segment cannot cross the plane (a
+// prism: cannot reach any face, all of which lie on the inner side), so intersectShadow finds
+// nothing in (eps, t_max). The margin (1e-3 plus 1e-6 of the scene's coordinate scale) is orders
+// above the rounding of the device's plane parameter (f32 dn, ~1e-7 relative). This drops walls,
+// floors and tunnel panels, which the boxes of interior cells meet but no segment crosses.
+//
+// Motion blur: with ypad > 0 the lists also serve the blur passes (bumped leaf boxes, "rectangle"
+// shapes shifted by |val| <= ypad in y): leaf boxes are padded by ypad in y, and a moving
+// rectangle's plane must clear the hull by ypad more.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <map>
 #include <vector>
@@ -67,13 +81,86 @@ bool swept_meets(const double clo[3], const double chi[3], const double llo[3], 
   return true;
 }
 
+// signed distances to the plane (p0, n) of the points of the boxes [alo, ahi] and [blo, bhi]:
+// [mn, mx] (false when n is degenerate)
+bool plane_range(const double* p0, const double* n, const double alo[3], const double ahi[3], const double blo[3],
+                 const double bhi[3], double& mn, double& mx)
+{
+  const double nn = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+  if (!(nn > 0) || !std::isfinite(nn)) return false;
+  const double c = n[0] * p0[0] + n[1] * p0[1] + n[2] * p0[2];
+  mn = INFINITY;
+  mx = -INFINITY;
+  for (int k = 0; k < 2; ++k) {
+    const double* lo = k ? blo : alo;
+    const double* hi = k ? bhi : ahi;
+    double smin = -c, smax = -c;
+    for (int a = 0; a < 3; ++a) {
+      smin += n[a] * (n[a] > 0 ? lo[a] : hi[a]);
+      smax += n[a] * (n[a] > 0 ? hi[a] : lo[a]);
+    }
+    mn = std::min(mn, smin / nn);
+    mx = std::max(mx, smax / nn);
+  }
+  return std::isfinite(mn) && std::isfinite(mx);
+}
+
+// no segment between the two boxes can make this shape's intersectShadow true (see the header)
+bool shape_separated(const dtd::DShapeHdr& h, const double* g, const double clo[3], const double chi[3],
+                     const double llo[3], const double lhi[3], double margin, double ypad)
+{
+  double mn, mx;
+  const double m = margin + ((h.flags & DT_F_NAMED_RECT) ? ypad : 0.0);
+  switch (h.type) {
+    case DT_SHAPE_RECTANGLE: {
+      const double* R = g + dtd::RC_R;
+      return plane_range(R + dtd::R_A, R + dtd::R_N, clo, chi, llo, lhi, mn, mx) && (mn > m || mx < -m);
+    }
+    case DT_SHAPE_CHECKERBOARD:
+    case DT_SHAPE_CHECKERBOARD_HOLE: {
+      const double* R = g + dtd::CK_R;
+      return plane_range(R + dtd::R_A, R + dtd::R_N, clo, chi, llo, lhi, mn, mx) && (mn > m || mx < -m);
+    }
+    case DT_SHAPE_TRIANGLE: {
+      const double* r1 = g + dtd::TR_R1;
+      const double* r2 = g + dtd::TR_R2;
+      const double n[3] = {r1[1] * r2[2] - r1[2] * r2[1], r1[2] * r2[0] - r1[0] * r2[2], r1[0] * r2[1] - r1[1] * r2[0]};
+      return plane_range(g + dtd::TR_A, n, clo, chi, llo, lhi, mn, mx) && (mn > m || mx < -m);
+    }
+    case DT_SHAPE_RECTPRISM_V2: {
+      // centroid: mean of the six face centres; a face plane with the hull strictly outside it
+      double cen[3] = {0, 0, 0};
+      for (int f = 0; f < 6; ++f) {
+        const double* R = g + dtd::PR_F + f * dtd::R_SIZE;
+        for (int a = 0; a < 3; ++a)
+          cen[a] += (R[dtd::R_A + a] + 0.5 * (R[dtd::R_V1N + a] * R[dtd::R_LEN1] + R[dtd::R_V2N + a] * R[dtd::R_LEN2])) / 6;
+      }
+      for (int f = 0; f < 6; ++f) {
+        const double* R = g + dtd::PR_F + f * dtd::R_SIZE;
+        const double* A = R + dtd::R_A;
+        const double* n = R + dtd::R_N;
+        const double nn = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        if (!(nn > 0)) continue;
+        const double side = ((cen[0] - A[0]) * n[0] + (cen[1] - A[1]) * n[1] + (cen[2] - A[2]) * n[2]) / nn;
+        if (!(std::fabs(side) > 1e-6)) continue;   // flat prism: no inner side
+        if (!plane_range(A, n, clo, chi, llo, lhi, mn, mx)) continue;
+        if ((side > 0 && mx < -m) || (side < 0 && mn > m)) return true;
+      }
+      return false;
+    }
+  }
+  return false;
+}
+
 }  // namespace
 
-bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const std::vector<dtd::DLight>& lights,
-                       ShadowGrid& g, double target_cells, float reach)
+bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene& fs, ShadowGrid& g,
+                       double target_cells, float reach, double ypad)
 {
+  const std::vector<dtd::DLight>& lights = fs.lights;
   g = ShadowGrid();
   g.reach = reach;
+  g.ypad = ypad;
   if (nodes.empty() || !(nodes[0].lb[0] <= nodes[0].ub[0])) return false;
   std::vector<int> leaves;
   for (size_t i = 0; i < nodes.size(); ++i)
@@ -135,6 +222,24 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const std::vecto
   for (int a = 0; a < 3; ++a) scale = std::max({scale, std::fabs(lo[a]), std::fabs(lo[a] + ext[a])});
   const double m1 = (reach + 0.05) * std::max({hh[0], hh[1], hh[2]}) + 1e-4 * (1 + scale);
   const double m2 = 2e-3 + 1e-4 * (1 + scale);
+  const double mplane = 1e-3 + 1e-6 * (1 + scale);
+  // leaf boxes, padded by ypad in y for the blur passes' bumped boxes
+  std::vector<std::array<double, 6>> lbox(nodes.size());
+  for (int leaf : leaves)
+    for (int a = 0; a < 3; ++a) {
+      lbox[leaf][a] = nodes[leaf].lb[a] - (a == 1 ? ypad : 0.0);
+      lbox[leaf][3 + a] = nodes[leaf].ub[a] + (a == 1 ? ypad : 0.0);
+    }
+  // shapes of each leaf (shape ids)
+  auto leaf_shapes = [&](int leaf, std::vector<int>& out) {
+    out.clear();
+    const dtd::DNodeDev& nd = nodes[leaf];
+    if (nd.meta & dtd::DN_SINGLE) out.push_back(nd.first);
+    else
+      for (int64_t q = 0; q < (int64_t)nd.aux; ++q) out.push_back(fs.bvh.leaf_idx[nd.first + q]);
+  };
+  std::vector<int> shp;
+  int dropped = 0;
 
   std::map<std::vector<int32_t>, uint32_t> uniq;
   std::vector<std::vector<int32_t>> lists(ncell);
@@ -160,8 +265,11 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const std::vecto
       // the light's own shape is skipped by the shadow test (cpp:832): a leaf holding only it
       // never occludes this light
       if ((nd.meta & dtd::DN_SINGLE) && nd.first == L.shape_index) continue;
+      const double* blo = lbox[leaf].data();
+      const double* bhi = lbox[leaf].data() + 3;
+      leaf_shapes(leaf, shp);
       int r0[3], r1[3];
-      for (int a = 0; a < 3; ++a) cell_range(lo[a], hh[a], g.dim[a], m1, llo[a], lhi[a], nd.lb[a], nd.ub[a], r0[a], r1[a]);
+      for (int a = 0; a < 3; ++a) cell_range(lo[a], hh[a], g.dim[a], m1, llo[a], lhi[a], blo[a], bhi[a], r0[a], r1[a]);
       for (int z = r0[2]; z <= r1[2]; ++z)
         for (int y = r0[1]; y <= r1[1]; ++y)
           for (int x = r0[0]; x <= r1[0]; ++x) {
@@ -171,7 +279,16 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const std::vecto
               clo[a] = lo[a] + ci[a] * hh[a] - m1;
               chi[a] = lo[a] + (ci[a] + 1) * hh[a] + m1;
             }
-            if (swept_meets(clo, chi, llo, lhi, nd.lb, nd.ub)) lists[(z * g.dim[1] + y) * g.dim[0] + x].push_back(leaf);
+            if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
+            bool sep = !shp.empty();
+            for (int sid : shp)
+              if (sid != L.shape_index &&
+                  !shape_separated(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, clo, chi, llo, lhi, mplane, ypad)) {
+                sep = false;
+                break;
+              }
+            if (sep) { ++dropped; continue; }
+            lists[(z * g.dim[1] + y) * g.dim[0] + x].push_back(leaf);
           }
     }
     g.base[l] = (int32_t)g.cells.size() / 2;
@@ -196,6 +313,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const std::vecto
     }
     g.n_lights = (int)l + 1;
   }
+  g.plane_dropped = dropped;
   return g.n_lights > 0;
 }
 
