@@ -48,10 +48,23 @@ double area(const double lb[3], const double ub[3])
 struct Builder {
   const std::vector<dtd::DNodeDev>& ref;   // reference tree, device format
   double ypad;                             // bump tree: leaf boxes padded by this in y
+  const double* eye;                       // children nearer to it first (null: SAH order)
   std::vector<LeafRef> leaves;
   std::vector<dtd::DNodeDev> out;
 
-  Builder(const std::vector<dtd::DNodeDev>& r, double yp) : ref(r), ypad(yp) {}
+  Builder(const std::vector<dtd::DNodeDev>& r, double yp, const double* e) : ref(r), ypad(yp), eye(e) {}
+
+  // squared distance from the eye to the box of ids[lo, hi)
+  double eye_dist2(const std::vector<int>& ids, int lo, int hi) const
+  {
+    double lb[3], ub[3], d2 = 0;
+    box_of(ids, lo, hi, lb, ub);
+    for (int a = 0; a < 3; ++a) {
+      const double d = eye[a] < lb[a] ? lb[a] - eye[a] : eye[a] > ub[a] ? eye[a] - ub[a] : 0.0;
+      d2 += d * d;
+    }
+    return d2;
+  }
 
   void box_of(const std::vector<int>& ids, int lo, int hi, double lb[3], double ub[3]) const
   {
@@ -120,8 +133,15 @@ struct Builder {
     nd.first = 0;
     nd.aux = 0;
     out[me] = nd;
-    build(ids, lo, best_split);
-    build(ids, best_split, hi);
+    // the walk visits the first child first: with an eye, the nearer one (camera rays then find
+    // their closest hit early and cull the boxes behind it). Order never changes the result.
+    if (eye && eye_dist2(ids, best_split, hi) < eye_dist2(ids, lo, best_split)) {
+      build(ids, best_split, hi);
+      build(ids, lo, best_split);
+    } else {
+      build(ids, lo, best_split);
+      build(ids, best_split, hi);
+    }
     out[me].skip = (int)out.size();
     return me;
   }
@@ -131,10 +151,11 @@ struct Builder {
 
 // ref: the reference tree in device format (pre-order, last child first, skip links).
 // Returns false (and leaves `out` empty) when the tree cannot carry 16-bit leaf ranks.
-bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNodeDev>& out, double ypad)
+bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNodeDev>& out, double ypad,
+                     const double* eye)
 {
   out.clear();
-  Builder b(ref, ypad);
+  Builder b(ref, ypad, eye);
   for (size_t i = 0; i < ref.size(); ++i) {
     if (!(ref[i].meta & dtd::DN_LEAF)) continue;
     LeafRef L;
