@@ -13,6 +13,7 @@ import json
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -51,28 +52,41 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     samples = 0
-    for n in mine:
+
+    def prepare(n):
+        """host side of frame n: buildFinal(n*8) from fresh globals, BVH, flatten, upload"""
+        torch.cuda.set_device(local)   # the HIP device is per thread
         f0 = time.perf_counter()
         g = dt.globals_default()   # fresh globals per frame (one process per frame in the reference)
         g.use_model = 0
         g.xRes, g.yRes, g.antialias_samples, g.max_depth = W, H, args.spp, args.depth
         built = dt.build_scene("final", n * 8, g)
         scene = dt.Scene(built, g)
-        f1 = time.perf_counter()
-        img = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
-        st = dt.render(scene, g, n * 8, img)
-        torch.cuda.synchronize()
-        f2 = time.perf_counter()
-        samples += st.samples
-        if args.per_frame:
-            print(json.dumps({"n": n, "frame": n * 8, "host_ms": round((f1 - f0) * 1e3, 1),
-                              "render_ms": round((f2 - f1) * 1e3, 1), "spp": st.samples // max(st.pixels, 1),
-                              "rays_per_sample": round(st.rays / max(st.samples, 1), 3),
-                              "sky_pixels": getattr(st, "sky_pixels", None)}), file=sys.stderr, flush=True)
-        if args.out:
-            os.makedirs(args.out, exist_ok=True)
-            dt.write_png(os.path.join(args.out, "frame.%04d.png" % n), g, img.cpu().numpy())
-        scene.close()
+        return g, scene, time.perf_counter() - f0
+
+    # frame n+1's host build runs on a worker thread while frame n renders (ctypes releases the
+    # GIL inside the library calls)
+    img = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    with ThreadPoolExecutor(1) as ex:
+        fut = ex.submit(prepare, mine[0]) if mine else None
+        for idx, n in enumerate(mine):
+            g, scene, host_s = fut.result()
+            if idx + 1 < len(mine):
+                fut = ex.submit(prepare, mine[idx + 1])
+            f1 = time.perf_counter()
+            st = dt.render(scene, g, n * 8, img)
+            torch.cuda.synchronize()
+            f2 = time.perf_counter()
+            samples += st.samples
+            if args.per_frame:
+                print(json.dumps({"n": n, "frame": n * 8, "host_ms": round(host_s * 1e3, 1),
+                                  "render_ms": round((f2 - f1) * 1e3, 1), "spp": st.samples // max(st.pixels, 1),
+                                  "rays_per_sample": round(st.rays / max(st.samples, 1), 3),
+                                  "sky_pixels": st.sky_pixels}), file=sys.stderr, flush=True)
+            if args.out:
+                os.makedirs(args.out, exist_ok=True)
+                dt.write_png(os.path.join(args.out, "frame.%04d.png" % n), g, img.cpu().numpy())
+            scene.close()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
