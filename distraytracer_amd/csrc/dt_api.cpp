@@ -243,7 +243,10 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
   {
     const char* bt = getenv("DT_BUMP_TREE");
     const double d = fabs((double)g->frame_range) * (1.0 + 1e-3) + 1e-3;
-    const double pad = ((double)fabsf(g->move_per_frame) * d + (double)fabsf(g->accel_t) * d * d * d) * 1.01 + 1e-6;
+    // DT_BUMP_PAD_SCALE (tests): shrink the pad so that some lanes exceed it and take the fallback
+    const char* bps = getenv("DT_BUMP_PAD_SCALE");
+    const double pad = (((double)fabsf(g->move_per_frame) * d + (double)fabsf(g->accel_t) * d * d * d) * 1.01 + 1e-6) *
+                       (bps ? atof(bps) : 1.0);
     s->bump_pad = (float)pad;
     if (!(bt && bt[0] == '0') && g->blur_samples > 0 && pad > 0 && pad < 1e3 && build_fast_tree(dnodes, bnodes, pad, eye))
       s->n_bnodes = (int)bnodes.size();

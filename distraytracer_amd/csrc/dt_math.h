@@ -30,7 +30,12 @@ DT_HD V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 DT_HD V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 DT_HD V3 mul(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
 DT_HD V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+#if defined(DT_ABL_FASTDIV) && defined(__HIP_DEVICE_COMPILE__)
+// diagnostic builds only (inexact): the cost bound of the three IEEE divisions of a V3 by a scalar
+DT_HD V3 divs(V3 a, double s) { const double r = __builtin_amdgcn_rcp(s); return v3(a.x * r, a.y * r, a.z * r); }
+#else
 DT_HD V3 divs(V3 a, double s) { return v3(a.x / s, a.y / s, a.z / s); }
+#endif
 DT_HD double dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 DT_HD V3 cross(V3 a, V3 b)
 {

@@ -233,6 +233,34 @@ def test_shadow_grid_matches_tree_walks(cuda, monkeypatch):
         assert np.array_equal(img, ref_img), (cells, reach)
 
 
+@pytest.mark.parametrize("n", [150, 210])
+def test_bump_tree_matches_reference_walks(cuda, monkeypatch, n):
+    """Motion-blur passes on the bump tree (host_fasttree.cpp: padded leaves, exact per-leaf
+    bumped gather with the ancestor chain) and on the blur-padded shadow-grid lists must give the
+    image of reference-tree walks bit for bit. Frame 1200 shifts by < 0.04, frame 1680 by up to 5
+    (bumped leaf boxes outgrow their parents: the ancestor-chain test). DT_BUMP_PAD_SCALE=0.5
+    pads for half the largest shift, so lanes beyond it send their waves to the reference walk.
+    Children order (DT_EYE_ORDER) must not matter either."""
+    g = dt.globals_default()
+    g.use_model = 0
+    built = dt.build_scene("final", n * 8, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = 320, 180, 16, 3
+    tile = dt.tiles(x0=96, y0=40, x1=224, y1=136)
+    monkeypatch.setenv("DT_BUMP_TREE", "0")
+    monkeypatch.setenv("DT_SHADOW_GRID", "0")
+    monkeypatch.setenv("DT_FAST_TREE", "0")
+    ref_img, ref_st = _render_gpu(built, g, n * 8, tile)
+    assert ref_st.rays > ref_st.samples   # blur passes ran
+    for env in ({}, {"DT_BUMP_PAD_SCALE": "0.5"}, {"DT_EYE_ORDER": "0"}):
+        for k in ("DT_BUMP_TREE", "DT_SHADOW_GRID", "DT_FAST_TREE", "DT_BUMP_PAD_SCALE", "DT_EYE_ORDER"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        img, st = _render_gpu(built, g, n * 8, tile)
+        assert st.rays == ref_st.rays and st.shadow_rays == ref_st.shadow_rays, env
+        assert np.array_equal(img, ref_img), env
+
+
 def _feature_scene():
     """A synthetic scene for the shading paths the shipped builders never use: a glass sphere
     (refraction + Fresnel, Q5), a steel mirror sphere, an Oren-Nayar sphere, a raw triangle, a

@@ -17,14 +17,14 @@ def main(path):
     lines = (m.group(0) if m else text).split("\n")
     inloop = collections.defaultdict(list)
     for i, line in enumerate(lines):
-        h = re.search(r"in Loop: Header=BB0_(\d+) Depth=(\d+)", line)
+        h = re.search(r"in Loop: Header=BB\d+_(\d+) Depth=(\d+)", line)
         if h:
             inloop[h.group(1)].append(i)
     rows = []
     for h, idx in inloop.items():
         a, b = min(idx), max(idx)
         j = b + 1
-        while j < len(lines) and not re.match(r"^\.LBB0_\d+:", lines[j]) and not lines[j].startswith("; %bb"):
+        while j < len(lines) and not re.match(r"^\.LBB\d+_\d+:", lines[j]) and not lines[j].startswith("; %bb"):
             j += 1
         body = lines[a:j]
         sc = sum(1 for x in body if "scratch_" in x)
