@@ -373,18 +373,25 @@ enum { P_DOF = 1, P_LIGHT = 2, P_SPHL = 3, P_GLOSSY = 4, P_BLUR = 5 };
 
 struct Rng {
   uint32_t k0, k1, pixel, sample;
-  __device__ void draw(uint32_t node, uint32_t purpose, uint32_t sub, double& u0, double& u1) const
+  __device__ void draw_words(uint32_t node, uint32_t purpose, uint32_t sub, uint32_t o[4]) const
   {
-    uint32_t o[4];
     // opaque key: the 10-round key schedule is recomputed per draw (20 SALU adds) instead of
     // being hoisted into 20 SGPRs that stay live across the whole kernel and spill
     uint32_t a = __builtin_amdgcn_readfirstlane(k0), b = __builtin_amdgcn_readfirstlane(k1);   // uniform key
     asm volatile("" : "+s"(a), "+s"(b));
     philox(pixel, sample, node, (purpose << 24) | sub, a, b, o);
+  }
+  __device__ void draw(uint32_t node, uint32_t purpose, uint32_t sub, double& u0, double& u1) const
+  {
+    uint32_t o[4];
+    draw_words(node, purpose, sub, o);
     u0 = u01(o[0], o[1]);
     u1 = u01(o[2], o[3]);
   }
 };
+
+// one 32-bit word as the float the reference gets from (float)uniform(generator)
+__device__ __forceinline__ float f01(uint32_t w) { return (float)((double)w * (1.0 / 4294967296.0)); }
 
 // =====================================================================================
 // primitives (geometry.cpp), geometry from the precomputed pool
@@ -1392,8 +1399,12 @@ __device__ __forceinline__ V3 sphere_light_sample(const Ctx& c, const DT_CAS DLi
 // light sampleRay (geometry.cpp:2751-2849)
 // xy: the area-light sample's float pair (rect_sample's (float)U draws). cache_mode 1 stores the
 // drawn pair there, 2 reuses the stored pair instead of drawing it again (same values).
+// Area lights 2k and 2k+1 share one draw (sub-index k): words 0-1 are light 2k's (x, y), words
+// 2-3 light 2k+1's. `pair` (pass 1) keeps words 2-3 of an even light's draw,
+// with pair[2] = the odd light they belong to, so the odd light does not draw again.
 __device__ __forceinline__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L, int li, V3 point, uint32_t node,
-                                           unsigned long long* st_sphl, float* xy = nullptr, int cache_mode = 0)
+                                           unsigned long long* st_sphl, float* xy = nullptr, int cache_mode = 0,
+                                           uint32_t* pair = nullptr)
 {
   if (L.type == DT_LIGHT_POINT) return sub(v3a(L.center), point);
   if (L.type == DT_LIGHT_RECT) {
@@ -1402,10 +1413,20 @@ __device__ __forceinline__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L,
       x = xy[0];
       y = xy[DT_WAVE];
     } else {
-      double u0, u1;
-      c.rng.draw(node, P_LIGHT, (uint32_t)li, u0, u1);
-      x = (float)u0;
-      y = (float)u1;
+      const bool odd = (li & 1) != 0;
+      uint32_t w0, w1;
+      if (odd && pair && pair[2] == (uint32_t)li) {
+        w0 = pair[0];
+        w1 = pair[1];
+      } else {
+        uint32_t o[4];
+        c.rng.draw_words(node, P_LIGHT, (uint32_t)li >> 1, o);
+        w0 = odd ? o[2] : o[0];
+        w1 = odd ? o[3] : o[1];
+        if (pair && !odd) { pair[0] = o[2]; pair[1] = o[3]; pair[2] = (uint32_t)li + 1u; }
+      }
+      x = f01(w0);
+      y = f01(w1);
       if (cache_mode == 1) { xy[0] = x; xy[DT_WAVE] = y; }
     }
     return sub(rect_sample_f(v3a(L.A), v3a(L.B), v3a(L.D), x, y), point);
@@ -1567,11 +1588,15 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
               for (int it = 0; it < 100000 && dot(sub(C, isectP), normal) <= 0; ++it) C = add(add(C, mul(0.1, wa)), mul(0.1, la));
               for (int it = 0; it < 100000 && dot(sub(D, isectP), normal) <= 0; ++it) D = add(add(D, mul(0.1, wa)), mul(0.1, la));
               const float kg = k_refl * k / P.brdf_samples;
+              // attempts 2a and 2a+1 of glossy sample i share one draw (sub-index (i << 8) | a):
+              // words 0-1 / 2-3 are their (x, y); gw keeps the odd attempt's words
+              uint32_t gw[2] = {0u, 0u};
               for (int i = 0; i < nref; i++) {
                 int attempt = 0;
-                double u0, u1;
-                c.rng.draw(node, P_GLOSSY, ((uint32_t)i << 8) | (uint32_t)attempt, u0, u1);
-                V3 sample_refl = sub(rect_sample(A, B, D, u0, u1), isectP);
+                uint32_t o[4];
+                c.rng.draw_words(node, P_GLOSSY, (uint32_t)i << 8, o);
+                gw[0] = o[2]; gw[1] = o[3];
+                V3 sample_refl = sub(rect_sample_f(A, B, D, f01(o[0]), f01(o[1])), isectP);
                 int sample_limit = 10;
                 bool exhausted = false;
                 while (dot(sample_refl, normal) <= 0) {
@@ -1579,8 +1604,15 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
                   float multiplier = (float)ldexp(1.0, 11 - sample_limit);   // pow(2, 11 - limit), exact
                   glossy_rect(refl_ray, isectP, multiplier, A, B, C, D, wv, lv);
                   attempt++;
-                  c.rng.draw(node, P_GLOSSY, ((uint32_t)i << 8) | (uint32_t)attempt, u0, u1);
-                  sample_refl = sub(rect_sample(A, B, D, u0, u1), isectP);
+                  float gx, gy;
+                  if (attempt & 1) {
+                    gx = f01(gw[0]); gy = f01(gw[1]);
+                  } else {
+                    c.rng.draw_words(node, P_GLOSSY, ((uint32_t)i << 8) | ((uint32_t)attempt >> 1), o);
+                    gx = f01(o[0]); gy = f01(o[1]);
+                    gw[0] = o[2]; gw[1] = o[3];
+                  }
+                  sample_refl = sub(rect_sample_f(A, B, D, gx, gy), isectP);
                   sample_limit--;
                 }
                 if (exhausted) atomicAdd(S.stats + ST_GLOSSY, 1ull);
@@ -1643,6 +1675,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       }
       asm volatile("" ::: "memory");
       uint32_t vis = 0;
+      uint32_t pair[3] = {0u, 0u, 0xffffffffu};   // area-light draw shared with the next light
       for (int li = 0; li < P.n_lights; ++li) {
         const DT_CAS DLight& L = cas(S.lights)[li];
         DT_CNT(9);
@@ -1653,7 +1686,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           // the first DT_LS_CACHE area lights park their sample pair in LDS for pass 2
           const bool cache = li < DT_LS_CACHE;
           sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL, cache ? &lsxy[cache ? li : 0][0][ln_] : nullptr,
-                              cache ? 1 : 0);
+                              cache ? 1 : 0, pair);
           t_max = (float)norm(sray);
           sn = normalized(sray);
           cnt.shadow++;

@@ -256,6 +256,9 @@ double or_u01(uint32_t w0, uint32_t w1)
   return ((double)(w0 >> 5) * 67108864.0 + (double)(w1 >> 6)) * (1.0 / 9007199254740992.0);
 }
 
+/* one word as a double in [0,1): the area-light (float)uniform draws */
+double or_u32_01(uint32_t w) { return (double)w * (1.0 / 4294967296.0); }
+
 static inline uint32_t fmix32(uint32_t h)
 {
   h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
@@ -279,6 +282,19 @@ static void rng2(const Rng* r, uint32_t node, uint32_t purpose, uint32_t sub, do
   or_philox4x32(ctr, r->key, o);
   *u0 = or_u01(o[0], o[1]);
   *u1 = or_u01(o[2], o[3]);
+}
+
+/* glossy sample i, attempt a: attempts 2k and 2k+1 share the draw with sub-index (i << 8) | k,
+   words 0-1 / 2-3, one word per (float)uniform */
+static void glossy_xy(const Rng* r, uint32_t node, int i, int attempt, double* u0, double* u1)
+{
+  uint32_t ctr[4] = {r->pixel, r->sample, node,
+                     ((uint32_t)P_GLOSSY << 24) | ((uint32_t)i << 8) | ((uint32_t)attempt >> 1)};
+  uint32_t o[4];
+  or_philox4x32(ctr, r->key, o);
+  const int k = (attempt & 1) * 2;
+  *u0 = or_u32_01(o[k]);
+  *u1 = or_u32_01(o[k + 1]);
 }
 
 /* ======================================================================= */
@@ -1151,9 +1167,13 @@ static V3 light_sample(const Ctx* c, int li, V3 point, uint32_t node)
   const dt_light_desc* L = &c->s->d->lights[li];
   if (L->type == DT_LIGHT_POINT) return sub(v3a(L->center), point);
   if (L->type == DT_LIGHT_RECT) {
-    double u0, u1;
-    rng2(&c->rng, node, P_LIGHT, (uint32_t)li, &u0, &u1);
-    return sub(rect_sample(v3a(L->A), v3a(L->B), v3a(L->D), u0, u1), point);
+    /* area lights 2k and 2k+1 share the draw with sub-index k: words 0-1 / 2-3, one word per
+       (float)uniform */
+    uint32_t ctr[4] = {c->rng.pixel, c->rng.sample, node, ((uint32_t)P_LIGHT << 24) | ((uint32_t)li >> 1)};
+    uint32_t o[4];
+    or_philox4x32(ctr, c->rng.key, o);
+    const int k = (li & 1) * 2;
+    return sub(rect_sample(v3a(L->A), v3a(L->B), v3a(L->D), or_u32_01(o[k]), or_u32_01(o[k + 1])), point);
   }
   /* sphereLight::sampleRay returns the sampled point itself (Q11) */
   V3 C = v3a(L->center);
@@ -1333,7 +1353,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
           int hit_tmp = 0;
           int attempt = 0;
           double u0, u1;
-          rng2(&c->rng, node, P_GLOSSY, ((uint32_t)i << 8) | (uint32_t)attempt, &u0, &u1);
+          glossy_xy(&c->rng, node, i, attempt, &u0, &u1);
           V3 sample_refl = sub(rect_sample(A, B, D, u0, u1), isectP);
           int sample_limit = 10;
           int exhausted = 0;
@@ -1342,7 +1362,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
             float multiplier = (float)pow(2, 11 - sample_limit);
             glossy_rect(refl_ray, isectP, multiplier, &A, &B, &C, &D, &wv, &lv);
             attempt++;
-            rng2(&c->rng, node, P_GLOSSY, ((uint32_t)i << 8) | (uint32_t)attempt, &u0, &u1);
+            glossy_xy(&c->rng, node, i, attempt, &u0, &u1);
             sample_refl = sub(rect_sample(A, B, D, u0, u1), isectP);
             sample_limit--;
           }

@@ -41,6 +41,7 @@ void or_cloud_color(const dt_globals* g, const double ray[3], const double origi
 /* counter RNG (shared definition with the device path) */
 void or_philox4x32(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 double or_u01(uint32_t w0, uint32_t w1);
+double or_u32_01(uint32_t w);   /* area-light draws: one word per float */
 
 /* renderImageCloud (cpp:1224-1279) on a pixel window / tile set */
 int or_render_sky(const dt_globals* g, float frame, const dt_tiles* tiles, float* out,

@@ -77,3 +77,13 @@ def test_u01_range():
     assert o.or_u01(0, 0) == 0.0
     top = o.or_u01(0xffffffff, 0xffffffff)
     assert top < 1.0 and top == (2 ** 53 - 1) / 2 ** 53
+
+
+def test_u32_01_range():
+    """one-word uniforms of the paired area-light draws: [0, 1), 2^-32 steps"""
+    o = oracle.oracle()
+    o.or_u32_01.restype = ctypes.c_double
+    o.or_u32_01.argtypes = [ctypes.c_uint32]
+    assert o.or_u32_01(0) == 0.0
+    assert o.or_u32_01(1) == 2.0 ** -32
+    assert o.or_u32_01(0xffffffff) == 1.0 - 2.0 ** -32
