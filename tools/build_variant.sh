@@ -7,7 +7,9 @@ C=$R/distraytracer_amd/csrc
 name=$1; src=$2; shift 2
 make -s -C "$C" >/dev/null
 mkdir -p "$R/distraytracer_amd/variants" "$C/build/var"
-/opt/rocm/bin/hipcc -I"$C" -DDT_TRACE_MIN_WAVES=${W:-4} "$@" --offload-arch=gfx950 -O3 -std=c++17 -fPIC \
+# the product's code-generation flags (Makefile CODEGEN) unless CODEGEN is set
+CG=${CODEGEN--mllvm -disable-machine-licm -mllvm -disable-machine-cse -mllvm -disable-machine-sink -mllvm -disable-licm-promotion}
+/opt/rocm/bin/hipcc -I"$C" -DDT_TRACE_MIN_WAVES=${W:-4} $CG "$@" --offload-arch=gfx950 -O3 -std=c++17 -fPIC \
   -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -c "$src" -o "$C/build/var/k_$name.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/distraytracer_amd/variants/libdt_$name.so" \
   "$C/build/var/k_$name.o" "$C"/build/dt_api.o "$C"/build/host_*.o
