@@ -56,7 +56,7 @@ using namespace dtd;
 #define DT_CLOUD_CHUNK 256
 #define DT_WAVE 64
 #ifndef DT_SLAB_MINMAX
-#define DT_SLAB_MINMAX 0   // min/max slab ends: exact, but measured 2% slower (register allocation)
+#define DT_SLAB_MINMAX 1   // min/max slab ends (exact with lb <= ub, P.boxes_ordered): +1% since the codegen flags
 #endif
 #ifndef DT_TCULL_HOIST
 #define DT_TCULL_HOIST 1
