@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <zlib.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -188,7 +189,18 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
   *out = nullptr;
   dt_scene* s = new dt_scene();
   std::string err;
+  // DT_TIMING=1: host stage times of the scene build on stderr
+  const bool timing = getenv("DT_TIMING") != nullptr;
+  auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double t_stage = now();
+  auto stage = [&](const char* name) {
+    if (!timing) return;
+    const double t = now();
+    fprintf(stderr, "dt_scene_create %-12s %8.2f ms\n", name, t - t_stage);
+    t_stage = t;
+  };
   int rc = flatten_scene(*desc, *g, s->flat, err);
+  stage("flatten+bvh");
   if (rc) {
     delete s;
     return fail(rc, err);
@@ -227,6 +239,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
   const char* eo = getenv("DT_EYE_ORDER");
   const double* eye = (eo && eo[0] == '0') ? nullptr : g->eye;
   if (!s->ftree_mode || !build_fast_tree(dnodes, fnodes, 0, eye)) fnodes.clear();
+  stage("fast tree");
   s->n_fnodes = (int)fnodes.size();
   s->boxes_ordered = 1;
   for (const auto* v : {&dnodes, &fnodes})
@@ -255,6 +268,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
   }
   if (bnodes.empty()) bnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
   if (bparent.empty()) bparent.push_back(-1);
+  stage("bump tree");
   // shadow grid (host_shadowgrid.cpp); DT_SHADOW_GRID=0: every shadow test walks a tree
   const char* sgv = getenv("DT_SHADOW_GRID");
   const char* sgc = getenv("DT_SG_CELLS");
@@ -280,6 +294,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
     dt_scene_destroy(s);
     return rc;
   }
+  stage("shadow grid");
   if ((rc = upload(dnodes, &s->d_nodes)) || (rc = upload(fnodes, &s->d_fnodes)) || (rc = upload(bnodes, &s->d_bnodes)) ||
       (rc = upload(bparent, &s->d_bparent)) || (rc = upload(leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
       (rc = upload(f.geom, &s->d_geom)) || (rc = upload(f.mat, &s->d_mat)) || (rc = upload(f.lights, &s->d_lights)) ||
@@ -295,6 +310,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
     dt_scene_destroy(s);
     return fail(DT_E_NO_DEVICE, "device allocation failed");
   }
+  stage("upload");
   *out = s;
   return DT_OK;
 }

@@ -27,8 +27,12 @@
 // rectangle's plane must clear the hull by ypad more.
 #include <algorithm>
 #include <array>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
-#include <map>
+#include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "host_internal.h"
@@ -238,10 +242,21 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
     else
       for (int64_t q = 0; q < (int64_t)nd.aux; ++q) out.push_back(fs.bvh.leaf_idx[nd.first + q]);
   };
-  std::vector<int> shp;
-  int dropped = 0;
+  long dropped = 0;
+  const bool timing = getenv("DT_TIMING") != nullptr;
+  auto now_ms = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const int hw_threads = (int)std::max(1u, std::thread::hardware_concurrency());
 
-  std::map<std::vector<int32_t>, uint32_t> uniq;
+  // identical lists are stored once (cells of one light, and across lights)
+  struct VecHash {
+    size_t operator()(const std::vector<int32_t>& v) const
+    {
+      uint64_t h = 1469598103934665603ull ^ v.size();
+      for (int32_t x : v) h = (h ^ (uint32_t)x) * 1099511628211ull;
+      return (size_t)h;
+    }
+  };
+  std::unordered_map<std::vector<int32_t>, uint32_t, VecHash> uniq;
   std::vector<std::vector<int32_t>> lists(ncell);
   for (size_t l = 0; l < lights.size() && l < (size_t)DT_MAX_SGRID; ++l) {
     const dtd::DLight& L = lights[l];
@@ -259,38 +274,60 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       llo[a] -= m2;
       lhi[a] += m2;
     }
+    const double t_light = now_ms();
     for (auto& v : lists) v.clear();
-    for (int leaf : leaves) {
-      const dtd::DNodeDev& nd = nodes[leaf];
-      // the light's own shape is skipped by the shadow test (cpp:832): a leaf holding only it
-      // never occludes this light
-      if ((nd.meta & dtd::DN_SINGLE) && nd.first == L.shape_index) continue;
-      const double* blo = lbox[leaf].data();
-      const double* bhi = lbox[leaf].data() + 3;
-      leaf_shapes(leaf, shp);
-      int r0[3], r1[3];
-      for (int a = 0; a < 3; ++a) cell_range(lo[a], hh[a], g.dim[a], m1, llo[a], lhi[a], blo[a], bhi[a], r0[a], r1[a]);
-      for (int z = r0[2]; z <= r1[2]; ++z)
-        for (int y = r0[1]; y <= r1[1]; ++y)
-          for (int x = r0[0]; x <= r1[0]; ++x) {
-            const int ci[3] = {x, y, z};
-            double clo[3], chi[3];
-            for (int a = 0; a < 3; ++a) {
-              clo[a] = lo[a] + ci[a] * hh[a] - m1;
-              chi[a] = lo[a] + (ci[a] + 1) * hh[a] + m1;
-            }
-            if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
-            bool sep = !shp.empty();
-            for (int sid : shp)
-              if (sid != L.shape_index &&
-                  !shape_separated(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, clo, chi, llo, lhi, mplane, ypad)) {
-                sep = false;
-                break;
+    // The (leaf, cell) tests run on worker threads, each owning a band of (z, y) cell rows. Every
+    // thread visits the leaves in the same order, so each cell's list comes out in leaf order, as
+    // from one thread.
+    const int rows = g.dim[1] * g.dim[2];
+    const int nthr = std::max(1, std::min({hw_threads, rows, 16}));
+    std::vector<long> dropped_t(nthr, 0);
+    auto work = [&](int t) {
+      const int row_lo = (int)((long)rows * t / nthr), row_hi = (int)((long)rows * (t + 1) / nthr);
+      std::vector<int> shp;
+      for (int leaf : leaves) {
+        const dtd::DNodeDev& nd = nodes[leaf];
+        // the light's own shape is skipped by the shadow test (cpp:832): a leaf holding only it
+        // never occludes this light
+        if ((nd.meta & dtd::DN_SINGLE) && (int32_t)nd.first == L.shape_index) continue;
+        const double* blo = lbox[leaf].data();
+        const double* bhi = lbox[leaf].data() + 3;
+        int r0[3], r1[3];
+        for (int a = 0; a < 3; ++a) cell_range(lo[a], hh[a], g.dim[a], m1, llo[a], lhi[a], blo[a], bhi[a], r0[a], r1[a]);
+        if (r0[0] > r1[0]) continue;
+        bool have_shapes = false;
+        for (int z = r0[2]; z <= r1[2]; ++z)
+          for (int y = r0[1]; y <= r1[1]; ++y) {
+            const int row = z * g.dim[1] + y;
+            if (row < row_lo || row >= row_hi) continue;
+            if (!have_shapes) { leaf_shapes(leaf, shp); have_shapes = true; }
+            for (int x = r0[0]; x <= r1[0]; ++x) {
+              const int ci[3] = {x, y, z};
+              double clo[3], chi[3];
+              for (int a = 0; a < 3; ++a) {
+                clo[a] = lo[a] + ci[a] * hh[a] - m1;
+                chi[a] = lo[a] + (ci[a] + 1) * hh[a] + m1;
               }
-            if (sep) { ++dropped; continue; }
-            lists[(z * g.dim[1] + y) * g.dim[0] + x].push_back(leaf);
+              if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
+              bool sep = !shp.empty();
+              for (int sid : shp)
+                if (sid != L.shape_index &&
+                    !shape_separated(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, clo, chi, llo, lhi, mplane, ypad)) {
+                  sep = false;
+                  break;
+                }
+              if (sep) { ++dropped_t[t]; continue; }
+              lists[(size_t)row * g.dim[0] + x].push_back(leaf);
+            }
           }
-    }
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nthr; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (auto& th : pool) th.join();
+    for (long d : dropped_t) dropped += d;
+    const double t_tests = now_ms();
     g.base[l] = (int32_t)g.cells.size() / 2;
     for (int c = 0; c < ncell; ++c) {
       std::vector<int32_t>& v = lists[c];
@@ -312,6 +349,9 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       g.cells.push_back((uint32_t)v.size());
     }
     g.n_lights = (int)l + 1;
+    if (timing)
+      fprintf(stderr, "  shadow grid light %zu: tests %.2f ms (%d threads), lists %.2f ms\n", l, t_tests - t_light, nthr,
+              now_ms() - t_tests);
   }
   g.plane_dropped = dropped;
   return g.n_lights > 0;
