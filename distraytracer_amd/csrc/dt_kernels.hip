@@ -64,6 +64,9 @@ using namespace dtd;
 #ifndef DT_FIN_PARTIAL
 #define DT_FIN_PARTIAL 1   // FINISH entries write/read only their colour and depth
 #endif
+#ifndef DT_ITEM_BATCH
+#define DT_ITEM_BATCH 2   // wave items per queue atomic (2: +0.4% on C3)
+#endif
 #ifndef DT_LS_CACHE
 #define DT_LS_CACHE 4   // lights whose area-sample pair is kept in LDS between the two light passes
 #endif
@@ -1915,11 +1918,16 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   for (int k = 0; k < 47; ++k) cnt.ph[k] = 0;
 #endif
 
+  int64_t item = 0, batch_end = 0;
   while (true) {
-    if (lane == 0) item_s = atomicAdd(S.queue, 1ull);
-    __syncthreads();
-    const int64_t item = (int64_t)item_s;
-    __syncthreads();
+    // items are dequeued DT_ITEM_BATCH at a time (one same-address atomic per batch)
+    if (item >= batch_end) {
+      if (lane == 0) item_s = atomicAdd(S.queue, (unsigned long long)DT_ITEM_BATCH);
+      __syncthreads();
+      item = (int64_t)item_s;
+      batch_end = item + DT_ITEM_BATCH;
+      __syncthreads();
+    }
     if (item >= P.n_items) break;
 
     const int group = P.ppw;
@@ -2042,6 +2050,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
       }
     }
+    ++item;
   }
   {
     unsigned long long r = wave_sum(cnt.rays), sh = wave_sum(cnt.shadow), tx = wave_sum(cnt.tex);
