@@ -157,6 +157,25 @@ def test_final_c5_tunnel_motion_blur(cuda, n):
     _cmp(gpu[m], ref[m], 0.003, "final C5 frame %d" % (n * 8))
 
 
+def test_final_c5_cloud_frame(cuda):
+    """C5 cloud frame buildFinal(2000) (n = 250 >= 244): the builder forces 1 spp and no aperture
+    (scene.h:795-796); 64 pixels per wave, each missing pixel's sky marched cooperatively."""
+    g = dt.globals_default()
+    g.use_model = 0
+    built = dt.build_scene("final", 2000, g)
+    assert g.antialias_samples == 1
+    g.xRes, g.yRes = 320, 180
+    x0, y0, x1, y1 = 128, 60, 176, 92
+    tile = dt.tiles(x0=x0, y0=y0, x1=x1, y1=y1)
+    gpu, st = _render_gpu(built, g, 2000, tile)
+    ref, rst = oracle.render(built, g, 2000, tile)
+    m = np.zeros((180, 320), dtype=bool)
+    m[180 - y1:180 - y0, x0:x1] = True
+    m = np.repeat(m.reshape(-1), 3)
+    assert st.samples == st.pixels == (x1 - x0) * (y1 - y0) and st.sky_pixels > 0
+    _cmp(gpu[m], ref[m], 0.0005, "final C5 cloud frame 2000")
+
+
 def test_final_c3_window(cuda):
     """C3 settings (1920x1080, 64 spp, depth 8) on a window around the window/sky region."""
     g = dt.globals_default()
