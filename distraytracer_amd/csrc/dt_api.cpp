@@ -449,18 +449,22 @@ static int enqueue_render(dt_scene* sc, const dtd::DParams& P, const std::vector
   hs.cloud_z = (const float*)sc->d_zs;
   hs.stats = sc->d_stats;
   hs.queue = sc->d_stats + ST_N;
+  static int resident = 0;
+  if (!resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
+  int64_t grid = P.n_items < resident ? P.n_items : resident;
+  if (grid < 1) grid = 1;
+  // two items per queue atomic pays when every wave takes many items (C3: ~500, +2%); with few
+  // (C2: ~30) the coarser tail costs more (-11%)
+  dtd::DParams PL = P;
+  PL.item_batch = PL.n_items >= 64 * grid ? 2 : 1;
   memset(sc->h_launch, 0, dt_launch_size());
   memcpy(sc->h_launch + dt_scene_struct_offset(), &hs, sizeof(hs));
-  memcpy(sc->h_launch + dt_params_struct_offset(), &P, sizeof(P));
+  memcpy(sc->h_launch + dt_params_struct_offset(), &PL, sizeof(PL));
   if (nz) HIPCHK(hipMemcpyAsync(sc->d_zs, sc->h_zs, nz * sizeof(float), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(sc->d_launch, sc->h_launch, dt_launch_size(), hipMemcpyHostToDevice, st));
   HIPCHK(hipEventRecord(sc->ev_copy, st));
   sc->copy_pending = true;
   HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 48), st));
-  static int resident = 0;
-  if (!resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
-  int64_t grid = P.n_items < resident ? P.n_items : resident;
-  if (grid < 1) grid = 1;
   HIPCHK(hipEventRecord(sc->ev0, st));
   HIPCHK(dt_launch_trace(sc->d_launch, out_dev, (int)grid, st));
   HIPCHK(hipEventRecord(sc->ev1, st));

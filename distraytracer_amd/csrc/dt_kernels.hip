@@ -65,7 +65,7 @@ using namespace dtd;
 #define DT_FIN_PARTIAL 1   // FINISH entries write/read only their colour and depth
 #endif
 #ifndef DT_ITEM_BATCH
-#define DT_ITEM_BATCH 2   // wave items per queue atomic (2: +0.4% on C3)
+#define DT_ITEM_BATCH 0   // wave items per queue atomic; 0: P.item_batch (host: 2 for long runs, else 1)
 #endif
 #ifndef DT_LS_CACHE
 #define DT_LS_CACHE 4   // lights whose area-sample pair is kept in LDS between the two light passes
@@ -1928,10 +1928,11 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   while (true) {
     // items are dequeued DT_ITEM_BATCH at a time (one same-address atomic per batch)
     if (item >= batch_end) {
-      if (lane == 0) item_s = atomicAdd(S.queue, (unsigned long long)DT_ITEM_BATCH);
+      const int batch = DT_ITEM_BATCH > 0 ? DT_ITEM_BATCH : (P.item_batch > 1 ? P.item_batch : 1);
+      if (lane == 0) item_s = atomicAdd(S.queue, (unsigned long long)batch);
       __syncthreads();
       item = (int64_t)item_s;
-      batch_end = item + DT_ITEM_BATCH;
+      batch_end = item + batch;
       __syncthreads();
     }
     if (item >= P.n_items) break;
