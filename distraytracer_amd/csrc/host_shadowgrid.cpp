@@ -41,6 +41,25 @@ namespace dth {
 
 namespace {
 
+// does the segment p -> q meet the box [lo, hi]? (list ordering only: not a correctness test)
+bool segment_meets_box(const double p[3], const double q[3], const double lo[3], const double hi[3])
+{
+  double t0 = 0.0, t1 = 1.0;
+  for (int a = 0; a < 3; ++a) {
+    const double d = q[a] - p[a];
+    if (std::fabs(d) < 1e-300) {
+      if (p[a] < lo[a] || p[a] > hi[a]) return false;
+      continue;
+    }
+    double ta = (lo[a] - p[a]) / d, tb = (hi[a] - p[a]) / d;
+    if (ta > tb) std::swap(ta, tb);
+    t0 = std::max(t0, ta);
+    t1 = std::min(t1, tb);
+    if (t0 > t1) return false;
+  }
+  return true;
+}
+
 // cells i in [0, n) whose interval [lo + i h - m, lo + (i+1) h + m], joined with the light
 // interval [llo, lhi], meets the leaf interval [a, b]
 void cell_range(double lo, double h, int n, double m, double llo, double lhi, double a, double b, int& i0,
@@ -244,6 +263,8 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   };
   long dropped = 0;
   const bool timing = getenv("DT_TIMING") != nullptr;
+  const char* so = getenv("DT_SG_ORDER");
+  const bool order_lists = so && atoi(so) != 0;   // opt-in: +0.6% on C3, +1.4 ms host build
   auto now_ms = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const int hw_threads = (int)std::max(1u, std::thread::hardware_concurrency());
 
@@ -274,6 +295,21 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       llo[a] -= m2;
       lhi[a] += m2;
     }
+    // light sample points for the list ordering: a point light, or a rectangle's centre and corners
+    double lpts[5][3];
+    int n_lpts = 1;
+    for (int a = 0; a < 3; ++a) {
+      if (L.type == DT_LIGHT_POINT) {
+        lpts[0][a] = L.center[a];
+      } else {
+        lpts[0][a] = 0.5 * (L.B[a] + L.D[a]);
+        lpts[1][a] = L.A[a];
+        lpts[2][a] = L.B[a];
+        lpts[3][a] = L.D[a];
+        lpts[4][a] = L.B[a] + L.D[a] - L.A[a];
+      }
+    }
+    if (L.type != DT_LIGHT_POINT) n_lpts = 5;
     const double t_light = now_ms();
     for (auto& v : lists) v.clear();
     // The (leaf, cell) tests run on worker threads, each owning a band of (z, y) cell rows. Every
@@ -320,6 +356,31 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
               lists[(size_t)row * g.dim[0] + x].push_back(leaf);
             }
           }
+      }
+      // Likely occluders first. The test is any-hit, so the order never changes an answer, but a
+      // lane stops testing at its first occluder and a wave leaves the list once all its lanes
+      // are occluded. Score: how many segments from the cell centre to the light's sample points
+      // (centre and corners) cross the leaf box; ties keep leaf order.
+      if (!order_lists) return;
+      std::vector<std::pair<int, int32_t>> keyed;
+      for (int row = row_lo; row < row_hi; ++row) {
+        const int y = row % g.dim[1], z = row / g.dim[1];
+        for (int x = 0; x < g.dim[0]; ++x) {
+          std::vector<int32_t>& v = lists[(size_t)row * g.dim[0] + x];
+          if (v.size() < 2 || (int)v.size() > DT_SGRID_MAX_LIST) continue;
+          const int ci[3] = {x, y, z};
+          double p[3];
+          for (int a = 0; a < 3; ++a) p[a] = lo[a] + (ci[a] + 0.5) * hh[a];
+          keyed.clear();
+          for (int32_t leaf : v) {
+            int s = 0;
+            for (int k = 0; k < n_lpts; ++k) s += segment_meets_box(p, lpts[k], lbox[leaf].data(), lbox[leaf].data() + 3);
+            keyed.push_back({-s, leaf});
+          }
+          std::stable_sort(keyed.begin(), keyed.end(),
+                           [](const std::pair<int, int32_t>& a, const std::pair<int, int32_t>& b) { return a.first < b.first; });
+          for (size_t k = 0; k < v.size(); ++k) v[k] = keyed[k].second;
+        }
       }
     };
     std::vector<std::thread> pool;
