@@ -285,10 +285,14 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
       sum += n;
       mx = std::max(mx, (size_t)n);
     }
+    uint64_t hash = 1469598103934665603ull;   // FNV-1a over cells and lists (A/B of build options)
+    for (auto x : s->sg.cells) hash = (hash ^ (uint32_t)x) * 1099511628211ull;
+    for (auto x : s->sg.list) hash = (hash ^ (uint32_t)x) * 1099511628211ull;
     fprintf(stderr, "shadow grid: lights %d dim %dx%dx%d cells %zu (tree %zu) mean list %.2f max %zu list pool %zu "
-            "plane-culled %ld ypad %g\n",
+            "plane-culled %ld ypad %g hash %016llx\n",
             s->sg.n_lights, s->sg.dim[0], s->sg.dim[1], s->sg.dim[2], cells, tree,
-            cells > tree ? (double)sum / (cells - tree) : 0.0, mx, s->sg.list.size(), s->sg.plane_dropped, s->sg.ypad);
+            cells > tree ? (double)sum / (cells - tree) : 0.0, mx, s->sg.list.size(), s->sg.plane_dropped, s->sg.ypad,
+            (unsigned long long)hash);
   }
   if ((rc = upload(s->sg.cells, &s->d_sg_cells)) || (rc = upload(s->sg.list, &s->d_sg_list))) {
     dt_scene_destroy(s);

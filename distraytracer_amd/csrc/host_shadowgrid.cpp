@@ -180,6 +180,7 @@ bool shape_separated(const dtd::DShapeHdr& h, const double* g, const double clo[
 bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene& fs, ShadowGrid& g,
                        double target_cells, float reach, double ypad)
 {
+  const double t_entry = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
   const std::vector<dtd::DLight>& lights = fs.lights;
   g = ShadowGrid();
   g.reach = reach;
@@ -190,7 +191,9 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
     if (nodes[i].meta & dtd::DN_LEAF) leaves.push_back((int)i);
   // large leaf counts (meshes): the per-leaf cell ranges would cost seconds of host time per
   // scene and the lists would overflow anyway; such scenes walk the tree
-  if (leaves.empty() || leaves.size() > 4096) return false;
+  // (DT_SG_MAX_LEAVES overrides the cap, for measurements)
+  const char* ml = getenv("DT_SG_MAX_LEAVES");
+  if (leaves.empty() || leaves.size() > (ml ? (size_t)atol(ml) : (size_t)4096)) return false;
   // Grid box: where the shading points are. A few giant shapes (C3's window-frame prisms span
   // y in [-996, 1004]) would stretch a box around everything into useless slabs. Per axis the
   // box is the hull of
@@ -264,7 +267,10 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   long dropped = 0;
   const bool timing = getenv("DT_TIMING") != nullptr;
   const char* so = getenv("DT_SG_ORDER");
-  const bool order_lists = so && atoi(so) != 0;   // opt-in: +0.6% on C3, +1.4 ms host build
+  const bool order_lists = so && atoi(so) != 0;
+  // DT_SG_BLOCK=0: per-cell tests only (the block tests are exact; kept for A/B)
+  const char* sb = getenv("DT_SG_BLOCK");
+  const bool block_cells = !sb || atoi(sb) != 0;   // opt-in: +0.6% on C3, +1.4 ms host build
   auto now_ms = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const int hw_threads = (int)std::max(1u, std::thread::hardware_concurrency());
 
@@ -279,6 +285,8 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   };
   std::unordered_map<std::vector<int32_t>, uint32_t, VecHash> uniq;
   std::vector<std::vector<int32_t>> lists(ncell);
+  const double t_setup = now_ms();
+  if (timing) fprintf(stderr, "  shadow grid setup: %.2f ms (%zu leaves, %d cells)\n", t_setup - t_entry, leaves.size(), ncell);
   for (size_t l = 0; l < lights.size() && l < (size_t)DT_MAX_SGRID; ++l) {
     const dtd::DLight& L = lights[l];
     g.base[l] = -1;
@@ -332,28 +340,47 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
         for (int a = 0; a < 3; ++a) cell_range(lo[a], hh[a], g.dim[a], m1, llo[a], lhi[a], blo[a], bhi[a], r0[a], r1[a]);
         if (r0[0] > r1[0]) continue;
         bool have_shapes = false;
+        // Cells go in blocks of BX x BY x 1. A cell's box lies inside its block's box, so when the
+        // block's swept box misses the leaf box, or all the leaf's shapes are separated from the
+        // block, the same holds for every cell in it. The lists come out as from per-cell tests
+        // (the margins m1 and mplane lie far above the rounding of the box corners).
+        const int BX = block_cells ? 8 : 1, BY = block_cells ? 4 : 1;
+        auto separated = [&](const double* clo, const double* chi) {
+          bool sep = !shp.empty();
+          for (int sid : shp)
+            if (sid != L.shape_index &&
+                !shape_separated(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, clo, chi, llo, lhi, mplane, ypad))
+              return false;
+          return sep;
+        };
+        auto cell_box = [&](int x0, int y0, int z0, int x1, int y1, int z1, double* clo, double* chi) {
+          const int c0[3] = {x0, y0, z0}, c1[3] = {x1, y1, z1};
+          for (int a = 0; a < 3; ++a) {
+            clo[a] = lo[a] + c0[a] * hh[a] - m1;
+            chi[a] = lo[a] + (c1[a] + 1) * hh[a] + m1;
+          }
+        };
         for (int z = r0[2]; z <= r1[2]; ++z)
-          for (int y = r0[1]; y <= r1[1]; ++y) {
-            const int row = z * g.dim[1] + y;
-            if (row < row_lo || row >= row_hi) continue;
+          for (int yb = r0[1]; yb <= r1[1]; yb += BY) {
+            const int ye = std::min(yb + BY - 1, r1[1]);
+            if (z * g.dim[1] + ye < row_lo || z * g.dim[1] + yb >= row_hi) continue;
             if (!have_shapes) { leaf_shapes(leaf, shp); have_shapes = true; }
-            for (int x = r0[0]; x <= r1[0]; ++x) {
-              const int ci[3] = {x, y, z};
+            for (int xb = r0[0]; xb <= r1[0]; xb += BX) {
+              const int xe = std::min(xb + BX - 1, r1[0]);
               double clo[3], chi[3];
-              for (int a = 0; a < 3; ++a) {
-                clo[a] = lo[a] + ci[a] * hh[a] - m1;
-                chi[a] = lo[a] + (ci[a] + 1) * hh[a] + m1;
-              }
+              cell_box(xb, yb, z, xe, ye, z, clo, chi);
               if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
-              bool sep = !shp.empty();
-              for (int sid : shp)
-                if (sid != L.shape_index &&
-                    !shape_separated(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, clo, chi, llo, lhi, mplane, ypad)) {
-                  sep = false;
-                  break;
+              const bool block_sep = separated(clo, chi);
+              for (int y = yb; y <= ye; ++y) {
+                const int row = z * g.dim[1] + y;
+                if (row < row_lo || row >= row_hi) continue;
+                for (int x = xb; x <= xe; ++x) {
+                  cell_box(x, y, z, x, y, z, clo, chi);
+                  if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
+                  if (block_sep || separated(clo, chi)) { ++dropped_t[t]; continue; }
+                  lists[(size_t)row * g.dim[0] + x].push_back(leaf);
                 }
-              if (sep) { ++dropped_t[t]; continue; }
-              lists[(size_t)row * g.dim[0] + x].push_back(leaf);
+              }
             }
           }
       }
@@ -415,6 +442,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
               now_ms() - t_tests);
   }
   g.plane_dropped = dropped;
+  if (timing) fprintf(stderr, "  shadow grid lights: %.2f ms\n", now_ms() - t_setup);
   return g.n_lights > 0;
 }
 
