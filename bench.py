@@ -111,10 +111,17 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    # ranks map onto the visible GPUs (identity on a full node; lets a 1-GPU box rehearse N>1)
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+    # one rank per GPU: RCCL refuses two ranks on one device, so a node with fewer GPUs than
+    # ranks is an error here, not something to fold onto fewer devices
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if local >= ndev:
+        raise SystemExit("bench.py: LOCAL_RANK %d but only %d visible GPU(s); run one rank per GPU" % (local, ndev))
     torch.cuda.set_device(local)
-    if world > 1:
+    # launched by torch.distributed.run (WORLD_SIZE set): the tile split + RCCL gather path runs at
+    # every world size, N=1 included (a 1-GPU box rehearses the collective code path that way)
+    distributed = "WORLD_SIZE" in os.environ
+    if distributed:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     g, built = build_globals(dt, args.config)
@@ -123,7 +130,7 @@ def main():
     W, H = g.xRes, g.yRes
     spp = int(int(g.antialias_samples ** 0.5) ** 2)
     dev = torch.device("cuda", local)
-    if world == 1:
+    if not distributed:
         image = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
         tile = dt.tiles()
     else:
@@ -138,17 +145,17 @@ def main():
     sh = stream.cuda_stream
 
     def finish_pending():
-        if world > 1:
+        if distributed:
             pipe.finish()
 
     def step(k, evs=None):
-        out = image if world == 1 else pipe.slab(k)
+        out = image if not distributed else pipe.slab(k)
         if evs is not None:
             evs[0].record(stream)
         dt.render_async(scene, g, 240, out, tile, stream=sh)
         if evs is not None:
             evs[1].record(stream)
-        if world > 1:
+        if distributed:
             pipe.submit(k)
 
     for k in range(args.warmup):
@@ -158,7 +165,7 @@ def main():
     stats = dt.collect_stats(scene, sh)
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -166,11 +173,11 @@ def main():
         step(k, evs[k])
     finish_pending()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -213,7 +220,7 @@ def main():
                                                                               g.brdf_samples),
                        "name": args.config, "use_model": int(g.use_model),
                        "frame": 240, "xRes": W, "yRes": H, "spp": spp, "max_depth": g.max_depth,
-                       "parallelism": "tile-split x%d + RCCL gather" % world if world > 1 else "single GPU"},
+                       "parallelism": "tile-split x%d + RCCL gather" % world if distributed else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 4), "peak": peak, "unit": "GB/s",
                          "frac": achieved / peak, "traffic": traffic,
                          "traffic_source": ("profiles/%s_summary.json (2*FETCH_SIZE + WRITE_SIZE, fabric requests "
@@ -239,7 +246,7 @@ def main():
             line["scene_bytes"] = flat_bytes
         print(json.dumps(line), flush=True)
     scene.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

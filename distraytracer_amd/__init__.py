@@ -14,12 +14,13 @@ an error (there is no CPU path in this package).
 """
 import ctypes
 
-from ._lib import (DATA_DIR, DT_OUT_IMAGE, DT_OUT_SLAB, BVHNode, DTError, Globals, SceneDesc, Stats,
-                   Tiles, check, lib)
+from ._lib import (DATA_DIR, DT_OUT_IMAGE, DT_OUT_SLAB, AccelInfo, BVHNode, DTError, Globals, SceneDesc,
+                   Stats, Tiles, check, lib)
 
 __all__ = ["Globals", "Tiles", "Stats", "DTError", "globals_default", "build_scene", "Scene",
            "render", "render_sky", "renderImage", "renderImageCloud", "write_ppm", "DATA_DIR",
-           "DT_OUT_IMAGE", "DT_OUT_SLAB", "slab_floats", "slab_floats_max", "unpack_slabs", "tiles", "check", "lib"]
+           "DT_OUT_IMAGE", "DT_OUT_SLAB", "slab_floats", "slab_floats_max", "unpack_slabs", "tiles", "check", "lib",
+           "accel_info"]
 
 
 def globals_default():
@@ -55,6 +56,16 @@ def build_scene(name, frame, g, data_dir=DATA_DIR):
     check(lib.dt_build_scene(name.encode(), float(frame), ctypes.byref(g), data_dir.encode(), ctypes.byref(out)),
           "dt_build_scene(%s)" % name)
     return BuiltScene(out)
+
+
+def accel_info(built, g):
+    """The acceleration structures dt_scene_create would upload (trees, shadow grid), built on the
+    host only: counts and content hashes (dt_accel_info_build). Build knobs are read from the
+    environment (DT_SG_BLOCK, DT_SG_ORDER, DT_FAST_TREE, ...) at call time."""
+    info = AccelInfo()
+    desc = built._ptr if isinstance(built, BuiltScene) else ctypes.pointer(built)
+    check(lib.dt_accel_info_build(desc, ctypes.byref(g), ctypes.byref(info)), "dt_accel_info_build")
+    return info.as_dict()
 
 
 class Scene:

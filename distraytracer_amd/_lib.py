@@ -95,11 +95,25 @@ class BVHNode(ctypes.Structure):
                 ("n_indices", c_int32), ("leaf", c_int32), ("depth", c_int32), ("lbound", D3), ("ubound", D3)]
 
 
+class AccelInfo(ctypes.Structure):
+    _fields_ = [("n_nodes", c_int32), ("n_fnodes", c_int32), ("n_bnodes", c_int32), ("boxes_ordered", c_int32),
+                ("sg_lights", c_int32), ("sg_dim", c_int32 * 3), ("sg_cells", c_int64), ("sg_tree_cells", c_int64),
+                ("sg_list_pool", c_int64), ("sg_list_entries", c_int64), ("nodes_hash", c_uint64),
+                ("fnodes_hash", c_uint64), ("bnodes_hash", c_uint64), ("sg_hash", c_uint64),
+                ("sg_contents_hash", c_uint64), ("bump_pad", c_float), ("sg_reach", c_float)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["sg_dim"] = tuple(self.sg_dim)
+        return d
+
+
 # every symbol include/dt.h declares (checked by tests/test_abi.py)
 EXPORTS = ["dt_abi_version", "dt_last_error", "dt_globals_default", "dt_scene_create", "dt_scene_destroy",
-           "dt_scene_bvh", "dt_bvh_build", "dt_slab_floats", "dt_slab_floats_max", "dt_render", "dt_render_async",
-           "dt_collect_stats", "dt_debug_counters", "dt_render_sky", "dt_unpack_slabs", "dt_build_scene", "dt_scene_desc_free",
-           "dt_write_ppm", "dt_write_png", "dt_mocap_bone_table"]
+           "dt_scene_bvh", "dt_bvh_build", "dt_accel_info_build", "dt_slab_floats", "dt_slab_floats_max",
+           "dt_render", "dt_render_async", "dt_collect_stats", "dt_debug_counters", "dt_render_sky",
+           "dt_unpack_slabs", "dt_build_scene", "dt_scene_desc_free", "dt_write_ppm", "dt_write_png",
+           "dt_mocap_bone_table"]
 
 
 class DTError(RuntimeError):
@@ -135,6 +149,7 @@ def _load():
                                    P(c_int32)]),
         "dt_bvh_build": (c_int32, [P(SceneDesc), P(Globals), P(BVHNode), c_int32, P(c_int32), c_int32, P(c_int32),
                                    P(c_int32)]),
+        "dt_accel_info_build": (c_int32, [P(SceneDesc), P(Globals), P(AccelInfo)]),
         "dt_slab_floats": (c_int64, [P(Globals), P(Tiles)]),
         "dt_slab_floats_max": (c_int64, [P(Globals), P(Tiles)]),
         "dt_render": (c_int32, [ctypes.c_void_p, P(Globals), c_int32, P(Tiles), ctypes.c_void_p, c_int32,

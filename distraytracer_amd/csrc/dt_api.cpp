@@ -210,97 +210,20 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
     return fail(DT_E_NO_DEVICE, "no HIP device");
   }
   const FlatScene& f = s->flat;
-  std::vector<int32_t> leaf = f.bvh.leaf_idx;
-  if (leaf.empty()) leaf.push_back(0);
-  std::vector<dtd::DNodeDev> dnodes(f.bvh.nodes.size());
-  for (size_t i = 0; i < dnodes.size(); ++i) {
-    const dtd::DNode& n = f.bvh.nodes[i];
-    dtd::DNodeDev& o = dnodes[i];
-    for (int a = 0; a < 3; ++a) { o.lb[a] = n.lb[a]; o.ub[a] = n.ub[a]; }
-    o.skip = n.skip;
-    o.meta = n.leaf ? dtd::DN_LEAF : 0u;
-    o.first = n.first;
-    o.aux = n.count;
-    if (n.leaf && n.count == 1) {
-      const dtd::DShapeHdr& h = f.hdr[f.bvh.leaf_idx[n.first]];
-      o.meta |= dtd::DN_SINGLE | ((uint32_t)h.type << 4) | ((h.flags & 0xffu) << 8);
-      o.first = f.bvh.leaf_idx[n.first];
-      o.aux = h.off;
-    }
-  }
-  // Alternative traversal tree (host_fasttree.cpp): exact by construction. Closest-hit walks use
-  // it by default; for shadow walks the reference's own SAH tree is faster on C3.
-  std::vector<dtd::DNodeDev> fnodes;
-  // DT_FAST_TREE: c (default) closest-hit walks, 1 every fast walk, s shadow walks only, 0 none.
-  // On C3 closest hit walks it faster (1666 vs 1624 Mpixel-samples/s), shadow walks slower.
-  const char* ft = getenv("DT_FAST_TREE");
-  s->ftree_mode = !ft ? 1 : ft[0] == '1' ? 3 : ft[0] == 'c' ? 1 : ft[0] == 's' ? 2 : 0;
-  // DT_EYE_ORDER=0: children in SAH order instead of nearer-to-the-camera first
-  const char* eo = getenv("DT_EYE_ORDER");
-  const double* eye = (eo && eo[0] == '0') ? nullptr : g->eye;
-  if (!s->ftree_mode || !build_fast_tree(dnodes, fnodes, 0, eye)) fnodes.clear();
-  stage("fast tree");
-  s->n_fnodes = (int)fnodes.size();
-  s->boxes_ordered = 1;
-  for (const auto* v : {&dnodes, &fnodes})
-    for (const dtd::DNodeDev& n : *v)
-      for (int a = 0; a < 3; ++a)
-        if (!(n.lb[a] <= n.ub[a])) s->boxes_ordered = 0;
-  if (fnodes.empty()) fnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
-  // Motion-blur bump tree: leaves padded by the largest |val| of cpp:1108-1135 for these globals
-  // (|move_per_frame| d + |accel_t| d^3 over d = frame_sample - frame in [0, frame_range], plus
-  // margin for the float evaluation). The device checks every lane's shift against the pad and
-  // walks the reference tree when one exceeds it. DT_BUMP_TREE=0 disables it.
-  std::vector<dtd::DNodeDev> bnodes;
-  std::vector<int32_t> bparent = tree_parents(dnodes);
-  {
-    const char* bt = getenv("DT_BUMP_TREE");
-    const double d = fabs((double)g->frame_range) * (1.0 + 1e-3) + 1e-3;
-    // DT_BUMP_PAD_SCALE (tests): shrink the pad so that some lanes exceed it and take the fallback
-    const char* bps = getenv("DT_BUMP_PAD_SCALE");
-    const double pad = (((double)fabsf(g->move_per_frame) * d + (double)fabsf(g->accel_t) * d * d * d) * 1.01 + 1e-6) *
-                       (bps ? atof(bps) : 1.0);
-    s->bump_pad = (float)pad;
-    if (!(bt && bt[0] == '0') && g->blur_samples > 0 && pad > 0 && pad < 1e3 && build_fast_tree(dnodes, bnodes, pad, eye))
-      s->n_bnodes = (int)bnodes.size();
-    else
-      bnodes.clear();
-  }
-  if (bnodes.empty()) bnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
-  if (bparent.empty()) bparent.push_back(-1);
-  stage("bump tree");
-  // shadow grid (host_shadowgrid.cpp); DT_SHADOW_GRID=0: every shadow test walks a tree
-  const char* sgv = getenv("DT_SHADOW_GRID");
-  const char* sgc = getenv("DT_SG_CELLS");
-  const char* sgr = getenv("DT_SG_REACH");
-  if ((sgv && sgv[0] == '0') ||
-      !build_shadow_grid(dnodes, f, s->sg, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : 0.5f,
-                         s->n_bnodes > 0 ? (double)s->bump_pad : 0.0))
-    s->sg = ShadowGrid();
-  if (getenv("DT_SG_VERBOSE")) {
-    size_t cells = s->sg.cells.size() / 2, tree = 0, sum = 0, mx = 0;
-    for (size_t c = 0; c < cells; ++c) {
-      const uint32_t n = s->sg.cells[2 * c + 1];
-      if (n == 0xffffffffu) { ++tree; continue; }
-      sum += n;
-      mx = std::max(mx, (size_t)n);
-    }
-    uint64_t hash = 1469598103934665603ull;   // FNV-1a over cells and lists (A/B of build options)
-    for (auto x : s->sg.cells) hash = (hash ^ (uint32_t)x) * 1099511628211ull;
-    for (auto x : s->sg.list) hash = (hash ^ (uint32_t)x) * 1099511628211ull;
-    fprintf(stderr, "shadow grid: lights %d dim %dx%dx%d cells %zu (tree %zu) mean list %.2f max %zu list pool %zu "
-            "plane-culled %ld ypad %g hash %016llx\n",
-            s->sg.n_lights, s->sg.dim[0], s->sg.dim[1], s->sg.dim[2], cells, tree,
-            cells > tree ? (double)sum / (cells - tree) : 0.0, mx, s->sg.list.size(), s->sg.plane_dropped, s->sg.ypad,
-            (unsigned long long)hash);
-  }
+  Accel acc;
+  build_accel(f, *g, acc, stage);
+  s->n_fnodes = acc.n_fnodes;
+  s->n_bnodes = acc.n_bnodes;
+  s->bump_pad = acc.bump_pad;
+  s->ftree_mode = acc.ftree_mode;
+  s->boxes_ordered = acc.boxes_ordered;
+  s->sg = std::move(acc.sg);
   if ((rc = upload(s->sg.cells, &s->d_sg_cells)) || (rc = upload(s->sg.list, &s->d_sg_list))) {
     dt_scene_destroy(s);
     return rc;
   }
-  stage("shadow grid");
-  if ((rc = upload(dnodes, &s->d_nodes)) || (rc = upload(fnodes, &s->d_fnodes)) || (rc = upload(bnodes, &s->d_bnodes)) ||
-      (rc = upload(bparent, &s->d_bparent)) || (rc = upload(leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
+  if ((rc = upload(acc.dnodes, &s->d_nodes)) || (rc = upload(acc.fnodes, &s->d_fnodes)) ||
+      (rc = upload(acc.bnodes, &s->d_bnodes)) || (rc = upload(acc.bparent, &s->d_bparent)) || (rc = upload(acc.leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
       (rc = upload(f.geom, &s->d_geom)) || (rc = upload(f.mat, &s->d_mat)) || (rc = upload(f.lights, &s->d_lights)) ||
       (rc = upload(f.tex, &s->d_tex))) {
     dt_scene_destroy(s);
@@ -372,6 +295,39 @@ int dt_bvh_build(const dt_scene_desc* desc, const dt_globals* g, dt_bvh_node* no
   FlatBVH b;
   build_bvh(*desc, *g, b);
   return export_bvh(b, nodes, cap, indices, index_cap, n_nodes, n_indices);
+}
+
+int dt_accel_info_build(const dt_scene_desc* desc, const dt_globals* g, dt_accel_info* info)
+{
+  if (!desc || !g || !info) return fail(DT_E_INVALID, "null argument");
+  if (desc->n_shapes < 0 || (desc->n_shapes > 0 && !desc->shapes)) return fail(DT_E_INVALID, "invalid descriptor");
+  FlatScene f;
+  std::string err;
+  int rc = flatten_scene(*desc, *g, f, err);
+  if (rc) return fail(rc, err);
+  Accel a;
+  build_accel(f, *g, a);
+  memset(info, 0, sizeof(*info));
+  info->n_nodes = (int32_t)a.dnodes.size();
+  info->n_fnodes = a.n_fnodes;
+  info->n_bnodes = a.n_bnodes;
+  info->boxes_ordered = a.boxes_ordered;
+  info->sg_lights = a.sg.n_lights;
+  for (int k = 0; k < 3; ++k) info->sg_dim[k] = a.sg.dim[k];
+  info->sg_cells = (int64_t)(a.sg.cells.size() / 2);
+  for (size_t c = 0; c + 1 < a.sg.cells.size(); c += 2) {
+    if (a.sg.cells[c + 1] == 0xffffffffu) info->sg_tree_cells++;
+    else info->sg_list_entries += a.sg.cells[c + 1];
+  }
+  info->sg_list_pool = (int64_t)a.sg.list.size();
+  info->nodes_hash = nodes_hash(a.dnodes);
+  info->fnodes_hash = a.n_fnodes ? nodes_hash(a.fnodes) : 0;
+  info->bnodes_hash = a.n_bnodes ? nodes_hash(a.bnodes) : 0;
+  info->sg_hash = sg_hash(a.sg, false);
+  info->sg_contents_hash = sg_hash(a.sg, true);
+  info->bump_pad = a.bump_pad;
+  info->sg_reach = a.sg.reach;
+  return DT_OK;
 }
 
 int64_t dt_slab_floats(const dt_globals* g, const dt_tiles* tiles)

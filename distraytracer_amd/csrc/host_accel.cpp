@@ -1,0 +1,154 @@
+// host_accel.cpp — every acceleration structure dt_scene_create uploads, built on the host with
+// no device: the reference-topology tree in device layout, the alternative closest-hit tree, the
+// motion-blur bump tree and the per-light shadow grid. dt_scene_create uploads the result;
+// dt_accel_info (CPU tests, A/B of build options) reports counts and content hashes of it.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "host_internal.h"
+
+namespace dth {
+
+bool sg_parse_block(const char* s, int& bx, int& by)
+{
+  bx = 8;
+  by = 4;
+  if (!s) return true;
+  if (strcmp(s, "0") == 0) {   // per-cell tests only (1 x 1 blocks)
+    bx = by = 1;
+    return true;
+  }
+  int x = 0, y = 0;
+  char tail = 0;
+  if (sscanf(s, "%dx%d%c", &x, &y, &tail) == 2 && x >= 1 && y >= 1) {
+    bx = x;
+    by = y;
+    return true;
+  }
+  return false;
+}
+
+void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::function<void(const char*)>& stage)
+{
+  a = Accel();
+  a.leaf = f.bvh.leaf_idx;
+  if (a.leaf.empty()) a.leaf.push_back(0);
+  std::vector<dtd::DNodeDev>& dnodes = a.dnodes;
+  dnodes.resize(f.bvh.nodes.size());
+  for (size_t i = 0; i < dnodes.size(); ++i) {
+    const dtd::DNode& n = f.bvh.nodes[i];
+    dtd::DNodeDev& o = dnodes[i];
+    for (int k = 0; k < 3; ++k) { o.lb[k] = n.lb[k]; o.ub[k] = n.ub[k]; }
+    o.skip = n.skip;
+    o.meta = n.leaf ? dtd::DN_LEAF : 0u;
+    o.first = n.first;
+    o.aux = n.count;
+    if (n.leaf && n.count == 1) {
+      const dtd::DShapeHdr& h = f.hdr[f.bvh.leaf_idx[n.first]];
+      o.meta |= dtd::DN_SINGLE | ((uint32_t)h.type << 4) | ((h.flags & 0xffu) << 8);
+      o.first = f.bvh.leaf_idx[n.first];
+      o.aux = h.off;
+    }
+  }
+  // Alternative traversal tree (host_fasttree.cpp): exact by construction. Closest-hit walks use
+  // it by default; for shadow walks the reference's own SAH tree is faster on C3.
+  // DT_FAST_TREE: c (default) closest-hit walks, 1 every fast walk, s shadow walks only, 0 none.
+  // On C3 closest hit walks it faster (1666 vs 1624 Mpixel-samples/s), shadow walks slower.
+  const char* ft = getenv("DT_FAST_TREE");
+  a.ftree_mode = !ft ? 1 : ft[0] == '1' ? 3 : ft[0] == 'c' ? 1 : ft[0] == 's' ? 2 : 0;
+  // DT_EYE_ORDER=0: children in SAH order instead of nearer-to-the-camera first
+  const char* eo = getenv("DT_EYE_ORDER");
+  const double* eye = (eo && eo[0] == '0') ? nullptr : g.eye;
+  if (!a.ftree_mode || !build_fast_tree(dnodes, a.fnodes, 0, eye)) a.fnodes.clear();
+  stage("fast tree");
+  a.n_fnodes = (int)a.fnodes.size();
+  a.boxes_ordered = 1;
+  for (const auto* v : {&a.dnodes, &a.fnodes})
+    for (const dtd::DNodeDev& n : *v)
+      for (int k = 0; k < 3; ++k)
+        if (!(n.lb[k] <= n.ub[k])) a.boxes_ordered = 0;
+  if (a.fnodes.empty()) a.fnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
+  // Motion-blur bump tree: leaves padded by the largest |val| of cpp:1108-1135 for these globals
+  // (|move_per_frame| d + |accel_t| d^3 over d = frame_sample - frame in [0, frame_range], plus
+  // margin for the float evaluation). The device checks every lane's shift against the pad and
+  // walks the reference tree when one exceeds it. DT_BUMP_TREE=0 disables it.
+  a.bparent = tree_parents(dnodes);
+  {
+    const char* bt = getenv("DT_BUMP_TREE");
+    const double d = fabs((double)g.frame_range) * (1.0 + 1e-3) + 1e-3;
+    // DT_BUMP_PAD_SCALE (tests): shrink the pad so that some lanes exceed it and take the fallback
+    const char* bps = getenv("DT_BUMP_PAD_SCALE");
+    const double pad = (((double)fabsf(g.move_per_frame) * d + (double)fabsf(g.accel_t) * d * d * d) * 1.01 + 1e-6) *
+                       (bps ? atof(bps) : 1.0);
+    a.bump_pad = (float)pad;
+    if (!(bt && bt[0] == '0') && g.blur_samples > 0 && pad > 0 && pad < 1e3 && build_fast_tree(dnodes, a.bnodes, pad, eye))
+      a.n_bnodes = (int)a.bnodes.size();
+    else
+      a.bnodes.clear();
+  }
+  if (a.bnodes.empty()) a.bnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
+  if (a.bparent.empty()) a.bparent.push_back(-1);
+  stage("bump tree");
+  // shadow grid (host_shadowgrid.cpp); DT_SHADOW_GRID=0: every shadow test walks a tree
+  const char* sgv = getenv("DT_SHADOW_GRID");
+  const char* sgc = getenv("DT_SG_CELLS");
+  const char* sgr = getenv("DT_SG_REACH");
+  if ((sgv && sgv[0] == '0') ||
+      !build_shadow_grid(dnodes, f, a.sg, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : 0.5f,
+                         a.n_bnodes > 0 ? (double)a.bump_pad : 0.0))
+    a.sg = ShadowGrid();
+  if (getenv("DT_SG_VERBOSE")) {
+    size_t cells = a.sg.cells.size() / 2, tree = 0, sum = 0, mx = 0;
+    for (size_t c = 0; c < cells; ++c) {
+      const uint32_t n = a.sg.cells[2 * c + 1];
+      if (n == 0xffffffffu) { ++tree; continue; }
+      sum += n;
+      mx = std::max(mx, (size_t)n);
+    }
+    fprintf(stderr, "shadow grid: lights %d dim %dx%dx%d cells %zu (tree %zu) mean list %.2f max %zu list pool %zu "
+            "plane-culled %ld ypad %g hash %016llx\n",
+            a.sg.n_lights, a.sg.dim[0], a.sg.dim[1], a.sg.dim[2], cells, tree,
+            cells > tree ? (double)sum / (cells - tree) : 0.0, mx, a.sg.list.size(), a.sg.plane_dropped, a.sg.ypad,
+            (unsigned long long)sg_hash(a.sg, false));
+  }
+  stage("shadow grid");
+}
+
+// FNV-1a over the cell records and lists in storage order, or (sorted) over each cell's list
+// contents only: the second is independent of list order (DT_SG_ORDER) and of how identical lists
+// are shared in the pool.
+uint64_t sg_hash(const ShadowGrid& sg, bool contents_only)
+{
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&h](uint32_t x) { h = (h ^ x) * 1099511628211ull; };
+  if (!contents_only) {
+    for (auto x : sg.cells) mix(x);
+    for (auto x : sg.list) mix((uint32_t)x);
+    return h;
+  }
+  std::vector<int32_t> tmp;
+  for (size_t c = 0; c + 1 < sg.cells.size(); c += 2) {
+    const uint32_t off = sg.cells[c], n = sg.cells[c + 1];
+    if (n == 0xffffffffu) { mix(0xffffffffu); continue; }
+    tmp.assign(sg.list.begin() + off, sg.list.begin() + off + n);
+    std::sort(tmp.begin(), tmp.end());
+    mix(n);
+    for (auto x : tmp) mix((uint32_t)x);
+  }
+  return h;
+}
+
+uint64_t nodes_hash(const std::vector<dtd::DNodeDev>& v)
+{
+  uint64_t h = 1469598103934665603ull;
+  for (const dtd::DNodeDev& n : v) {
+    const unsigned char* p = (const unsigned char*)&n;
+    for (size_t i = 0; i < sizeof(n); ++i) h = (h ^ p[i]) * 1099511628211ull;
+  }
+  return h;
+}
+
+}  // namespace dth

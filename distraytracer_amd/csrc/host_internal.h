@@ -1,5 +1,7 @@
 // host_internal.h — host-side pieces of libdt (not part of the C ABI).
 #pragma once
+#include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -52,6 +54,28 @@ struct FlatScene {
   std::vector<uint8_t> tex;
 };
 int flatten_scene(const dt_scene_desc& d, const dt_globals& g, FlatScene& out, std::string& err);
+
+// DT_SG_BLOCK: null -> 8x4 (default), "0" -> 1x1 (per-cell tests), "XxY" with X, Y >= 1; false
+// (and the default) for anything else
+bool sg_parse_block(const char* s, int& bx, int& by);
+
+// host_accel.cpp: everything dt_scene_create uploads besides the flat scene, built without a device
+struct Accel {
+  std::vector<dtd::DNodeDev> dnodes;   // reference tree, device layout
+  std::vector<dtd::DNodeDev> fnodes;   // alternative closest-hit tree (1 dummy node when n_fnodes == 0)
+  std::vector<dtd::DNodeDev> bnodes;   // motion-blur bump tree (1 dummy node when n_bnodes == 0)
+  std::vector<int32_t> bparent;        // parent of every reference node
+  std::vector<int32_t> leaf;           // leaf_idx (never empty)
+  int n_fnodes = 0, n_bnodes = 0;
+  float bump_pad = 0;
+  int ftree_mode = 0;
+  int boxes_ordered = 0;
+  ShadowGrid sg;
+};
+void build_accel(const FlatScene& f, const dt_globals& g, Accel& a,
+                 const std::function<void(const char*)>& stage = [](const char*) {});
+uint64_t sg_hash(const ShadowGrid& sg, bool contents_only);
+uint64_t nodes_hash(const std::vector<dtd::DNodeDev>& v);
 
 // camera / params (host_flatten.cpp)
 int fill_params(const dt_globals& g, int frame, const dt_tiles* tiles, dtd::DParams& P, std::string& err);

@@ -486,7 +486,6 @@ int load_ad_frame(OwnedDesc& O, int idx)
 void triangle_prism_mesh(OwnedDesc& O, const dt_globals& g, V3 a_cap0, V3 b_cap0, V3 c_cap0, V3 a_cap1, V3 b_cap1,
                          V3 c_cap1, int time_frame, bool texture, bool motion)
 {
-  static std::mt19937 gen(0);   // scene.h:57, reseeded per rectangle
   std::uniform_int_distribution<> unif(0, kAdFrames - 1000);
   const V3 eye = v3a(g.eye);
   const float far = g.far_dist;
@@ -514,7 +513,7 @@ void triangle_prism_mesh(OwnedDesc& O, const dt_globals& g, V3 a_cap0, V3 b_cap0
   const V3 adj_b0 = add(b_cap0, divs(mul(bounding_width, bc_v), 2));
   int seed_counter = 0;
   auto place = [&](V3 a, V3 b, V3 c, V3 d, V3 dir, int i, uint32_t seed) {
-    gen.seed(seed);
+    std::mt19937 gen(seed);   // scene.h:57, reseeded per rectangle (local: dt_build_scene stays reentrant)
     const int frame_ind = unif(gen) + (time_frame - g.frame_prism);
     const int tex_index = load_ad_frame(O, frame_ind);
     const V3 off = mul((double)i, mul(bounding_width + rect_height, dir));

@@ -266,17 +266,14 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   };
   long dropped = 0;
   const bool timing = getenv("DT_TIMING") != nullptr;
+  // DT_SG_ORDER=1: lists ordered likely-occluder first. Opt-in: +0.6% on C3, +1.4 ms host build
+  // 
   const char* so = getenv("DT_SG_ORDER");
   const bool order_lists = so && atoi(so) != 0;
-  // DT_SG_BLOCK=0: per-cell tests only; DT_SG_BLOCK=XxY: blocks of X x Y cells (the block tests
-  // are exact; the knob is for A/B)
   int blk_x = 8, blk_y = 4;
-  if (const char* sb = getenv("DT_SG_BLOCK")) {
-    if (sscanf(sb, "%dx%d", &blk_x, &blk_y) != 2) blk_x = blk_y = atoi(sb) != 0 ? 0 : 1;
-    if (blk_x == 0) { blk_x = 8; blk_y = 4; }
-    blk_x = std::max(1, blk_x);
-    blk_y = std::max(1, blk_y);
-  }   // opt-in: +0.6% on C3, +1.4 ms host build
+  if (!sg_parse_block(getenv("DT_SG_BLOCK"), blk_x, blk_y))
+    fprintf(stderr, "dt: DT_SG_BLOCK='%s' not understood (use 0 or XxY with X, Y >= 1): default 8x4\n",
+            getenv("DT_SG_BLOCK"));
   auto now_ms = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const int hw_threads = (int)std::max(1u, std::thread::hardware_concurrency());
 

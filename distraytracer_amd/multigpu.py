@@ -24,7 +24,7 @@ class FrameSplit:
         """gather the per-rank slabs into `gathered` (world*slab_floats) on rank 0. With
         async_op the collective's Work is returned (wait() before reading `gathered`)."""
         import torch.distributed as dist
-        if self.world == 1:
+        if self.world == 1 and not (dist.is_available() and dist.is_initialized()):
             gathered.copy_(slab)
             return None
         parts = list(gathered.view(self.world, self.slab_floats).unbind(0)) if self.rank == 0 else None

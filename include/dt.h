@@ -250,6 +250,21 @@ int  dt_scene_bvh(const dt_scene* s, dt_bvh_node* nodes, int32_t cap,
 int  dt_bvh_build(const dt_scene_desc* desc, const dt_globals* g, dt_bvh_node* nodes, int32_t cap,
                   int32_t* indices, int32_t index_cap, int32_t* n_nodes, int32_t* n_indices);
 
+/* The acceleration structures dt_scene_create would upload for (desc, g), built on the host
+ * only (no device): counts and FNV-1a content hashes, for A/B checks of build options
+ * (DT_SG_BLOCK, DT_SG_ORDER, ...). No reference counterpart: the reference walks its own BVH
+ * (helpers.h:381-472, geometry.cpp:2657-2740) and has no shadow grid. */
+typedef struct dt_accel_info {
+  int32_t n_nodes, n_fnodes, n_bnodes, boxes_ordered;
+  int32_t sg_lights, sg_dim[3];
+  int64_t sg_cells, sg_tree_cells, sg_list_pool, sg_list_entries;
+  uint64_t nodes_hash, fnodes_hash, bnodes_hash;
+  uint64_t sg_hash;            /* cells + list pool in storage order */
+  uint64_t sg_contents_hash;   /* each cell's list as a sorted set (order-free) */
+  float bump_pad, sg_reach;
+} dt_accel_info;
+int dt_accel_info_build(const dt_scene_desc* desc, const dt_globals* g, dt_accel_info* info);
+
 /* number of floats a DT_OUT_SLAB output needs for (g, tiles) */
 int64_t dt_slab_floats(const dt_globals* g, const dt_tiles* tiles);
 int64_t dt_slab_floats_max(const dt_globals* g, const dt_tiles* tiles); /* max over ranks */

@@ -36,7 +36,7 @@ def test_abi_version():
 
 STRUCTS = {"dt_globals": _lib.Globals, "dt_shape_desc": _lib.ShapeDesc, "dt_light_desc": _lib.LightDesc,
            "dt_texture_desc": _lib.TextureDesc, "dt_scene_desc": _lib.SceneDesc, "dt_tiles": _lib.Tiles,
-           "dt_stats": _lib.Stats, "dt_bvh_node": _lib.BVHNode}
+           "dt_stats": _lib.Stats, "dt_bvh_node": _lib.BVHNode, "dt_accel_info": _lib.AccelInfo}
 
 
 def test_struct_layout_matches_c(tmp_path):

@@ -243,13 +243,20 @@ def test_shadow_grid_matches_tree_walks(cuda, monkeypatch):
     tile = dt.tiles(x0=900, y0=500, x1=964, y1=548)
     monkeypatch.setenv("DT_SHADOW_GRID", "0")
     ref_img, ref_st = _render_gpu(built, g, 240, tile)
-    for cells, reach in (("32768", "0.5"), ("4096", "2")):
+    # grid size/reach, the block-test sizes of the host build (tests/test_host.py checks the lists
+    # themselves) and the likely-occluder list order (any-hit: the image must not change)
+    variants = [{"DT_SG_CELLS": "32768", "DT_SG_REACH": "0.5"}, {"DT_SG_CELLS": "4096", "DT_SG_REACH": "2"}]
+    variants += [{"DT_SG_BLOCK": b, "DT_SG_ORDER": o} for b in ("0", "4x2", "32x8") for o in ("0", "1")]
+    variants += [{"DT_SG_ORDER": "1"}]
+    for env in variants:
+        for k in ("DT_SG_CELLS", "DT_SG_REACH", "DT_SG_BLOCK", "DT_SG_ORDER"):
+            monkeypatch.delenv(k, raising=False)
         monkeypatch.setenv("DT_SHADOW_GRID", "1")
-        monkeypatch.setenv("DT_SG_CELLS", cells)
-        monkeypatch.setenv("DT_SG_REACH", reach)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         img, st = _render_gpu(built, g, 240, tile)
-        assert st.shadow_rays == ref_st.shadow_rays
-        assert np.array_equal(img, ref_img), (cells, reach)
+        assert st.shadow_rays == ref_st.shadow_rays, env
+        assert np.array_equal(img, ref_img), env
 
 
 @pytest.mark.parametrize("n", [150, 210])

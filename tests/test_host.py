@@ -2,6 +2,7 @@
 vs the oracle's independent restatement of helpers.h:330-472), tile ownership and slab
 scatter, and analytic anchors of the oracle renderer."""
 import collections
+import ctypes
 
 import numpy as np
 import pytest
@@ -150,3 +151,70 @@ def test_oracle_sky_image_cloud_anchor():
     g.xRes, g.yRes = 64, 48
     img = oracle.render_sky(g, 1.0, dt.tiles())
     assert np.isfinite(img).all() and img.min() >= 0 and img.max() <= 255
+
+
+# ---- acceleration structures built on the host (dt_accel_info_build) ------------------------
+
+def _accel(name, frame, models, env, monkeypatch):
+    for k in ("DT_SG_BLOCK", "DT_SG_ORDER"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = dt.globals_default()
+    g.use_model = models
+    b = dt.build_scene("final", frame, g)
+    return dt.accel_info(b, g)
+
+
+# C3's room, C4's meshes (2442 leaves), a C5 tunnel frame with blur-padded lists
+ACCEL_SCENES = [("c3", 240, 0), ("c4", 240, 1), ("c5-tunnel", 1200, 0)]
+
+
+@pytest.mark.parametrize("name,frame,models", ACCEL_SCENES, ids=[s[0] for s in ACCEL_SCENES])
+def test_shadow_grid_block_tests_give_identical_lists(name, frame, models, monkeypatch):
+    """The per-block (leaf, cell) rejection (host_shadowgrid.cpp) is exact only while the swept
+    test and the plane separation stay monotone in the cell box: every block size must give the
+    per-cell build's lists bit for bit (cells, counts and pool, in storage order)."""
+    base = _accel(name, frame, models, {"DT_SG_BLOCK": "0"}, monkeypatch)
+    assert base["sg_lights"] > 0 and base["sg_list_entries"] > 0
+    for blk in ("4x2", "8x4", "32x8", "1x1"):
+        got = _accel(name, frame, models, {"DT_SG_BLOCK": blk}, monkeypatch)
+        assert got["sg_hash"] == base["sg_hash"], blk
+        assert got["sg_list_entries"] == base["sg_list_entries"], blk
+    dflt = _accel(name, frame, models, {}, monkeypatch)
+    assert dflt["sg_hash"] == base["sg_hash"]
+    assert dflt["nodes_hash"] == base["nodes_hash"] and dflt["fnodes_hash"] == base["fnodes_hash"]
+
+
+@pytest.mark.parametrize("name,frame,models", ACCEL_SCENES[:1] + ACCEL_SCENES[2:],
+                         ids=[ACCEL_SCENES[0][0], ACCEL_SCENES[2][0]])
+def test_shadow_grid_ordered_lists_hold_the_same_leaves(name, frame, models, monkeypatch):
+    """DT_SG_ORDER=1 reorders each cell's list (likely occluder first) and nothing else."""
+    plain = _accel(name, frame, models, {}, monkeypatch)
+    ordered = _accel(name, frame, models, {"DT_SG_ORDER": "1"}, monkeypatch)
+    assert ordered["sg_contents_hash"] == plain["sg_contents_hash"]
+    assert ordered["sg_list_entries"] == plain["sg_list_entries"]
+    assert ordered["sg_cells"] == plain["sg_cells"] and ordered["sg_tree_cells"] == plain["sg_tree_cells"]
+
+
+def test_shadow_grid_block_knob_is_strict(monkeypatch, capfd):
+    """Malformed DT_SG_BLOCK values are reported and fall back to the default 8x4 blocks."""
+    dflt = _accel("c3", 240, 0, {}, monkeypatch)
+    capfd.readouterr()
+    for bad in ("1", "8", "0x4", "8x", "x4", "8x4junk"):
+        got = _accel("c3", 240, 0, {"DT_SG_BLOCK": bad}, monkeypatch)
+        assert got["sg_hash"] == dflt["sg_hash"]
+        assert "DT_SG_BLOCK" in capfd.readouterr().err, bad
+
+
+def test_accel_info_matches_scene_bvh():
+    """dt_accel_info_build builds the tree dt_bvh_build exports (same node count)."""
+    g, b = final240()
+    info = dt.accel_info(b, g)
+    nodes = (dt.BVHNode * 4096)()
+    idx = (ctypes.c_int32 * 4096)()
+    nn, ni = ctypes.c_int32(), ctypes.c_int32()
+    dt.check(dt.lib.dt_bvh_build(b._ptr, ctypes.byref(g), nodes, 4096, idx, 4096, ctypes.byref(nn),
+                                 ctypes.byref(ni)), "dt_bvh_build")
+    assert info["n_nodes"] == nn.value
+    assert info["boxes_ordered"] == 1 and info["n_fnodes"] == info["n_nodes"]
