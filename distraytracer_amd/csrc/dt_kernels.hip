@@ -955,6 +955,15 @@ __device__ __forceinline__ bool box_hit_finite(const DNodeDev& b, const RayBox& 
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+__device__ __forceinline__ unsigned long long wave_sum(uint32_t v)
+{
+  unsigned long long x = v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+
 // wave-uniform traversal state shared by closest_hit / occluded
 struct Walk {
   RayBox rb;
@@ -1250,6 +1259,43 @@ __device__ bool occluded_list(const DScene& S, const Walk& w, bool active, V3 bs
   return occl;
 }
 
+// wave minimum of a per-lane int (DPP/swizzle butterfly; every lane gets the result)
+__device__ __forceinline__ int wave_min_i32(int v)
+{
+#pragma unroll
+  for (int o = 1; o < DT_WAVE; o <<= 1) v = min(v, __shfl_xor(v, o, DT_WAVE));
+  return v;
+}
+
+// Scattered waves (lanes in different grid cells): each lane's own cell list holds every leaf that
+// can occlude it, so the wave tests the union of its lanes' lists -- merged in leaf order (the
+// lists are sorted by leaf index, built in leaf order), each leaf once, with the same exact box
+// test and shape tests as the walk. A lane testing a leaf outside its own list is harmless: the
+// box and shape tests are the reference's own, the list only bounds where an occluder can be.
+template <bool BUMP, class CNT>
+__device__ bool occluded_union(const DScene& S, const Walk& w, bool active, V3 bstart, V3 sn, V3 sstart, float t_max,
+                               int skip_shape, float shift, uint32_t off, uint32_t n, CNT& cnt)
+{
+  bool occl = false;
+  const float tcull = shadow_tcull(t_max);
+  uint32_t k = 0;
+  int head = (active && n > 0) ? S.sg_list[off] : INT_MAX;
+  while (true) {
+    const int m = uni(wave_min_i32(occl ? INT_MAX : head));
+    if (m == INT_MAX) break;
+    const DNodeDev nd = cas(S.nodes)[m];
+    const bool hb = active & !occl &
+                    (BUMP ? bump_leaf_gathered(S, w, m, shift, bstart) : node_hit<false>(w, nd, 0.0f, bstart, tcull));
+    DT_CNT(34);
+    if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, shift, cnt);
+    if (head == m) {
+      ++k;
+      head = k < n ? S.sg_list[off + k] : INT_MAX;
+    }
+  }
+  return occl;
+}
+
 // shading point in grid-cell coordinates
 __device__ __forceinline__ void sg_coords(const DParams& P, V3 p, float& x, float& y, float& z)
 {
@@ -1273,9 +1319,11 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
 #endif
   // Shadow grid: the first active lane's cell serves every lane within sg_reach cells of it.
   // Waves whose lanes all lie within that reach (coherent primary bounces) test the cell's
-  // candidate list; scattered waves walk the tree. Measured no better for scattered waves: a
-  // second union list; per-lane lists (each lane its own cell's list, vector loads and a
-  // per-lane shape switch: C3 1725 vs 1932, C4 843 vs 936 Mpixel-samples/s).
+  // candidate list. Scattered waves (mostly glossy bounces) test the union of their lanes' own
+  // cell lists, merged in leaf order (C3: 4.8 leaves per union against ~24 node visits per tree
+  // walk); a wave with a lane outside the grid or in a cell whose list is too long walks the tree.
+  // Measured slower for scattered waves: per-lane list walks with a per-lane shape switch (C3 1725
+  // vs 1932, C4 843 vs 936 Mpixel-samples/s), the lists of two cells in turn.
   if (li < P.sg_n && P.sg_base[li] >= 0) {
     const unsigned long long am = __ballot(active);
     if (!am) return false;
@@ -1302,6 +1350,28 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       }
       DT_CNT(37);
     }
+#ifndef DT_NO_SG_UNION
+    {   // scattered waves: the union of the lanes' own cell lists, when every lane has one
+      const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
+      bool lin = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.sg_dim[0] && fy < (float)P.sg_dim[1] &&
+                 fz < (float)P.sg_dim[2];
+      uint32_t loff = 0, ln = 0;
+      if (active && lin) {
+        const int cl = ((int)fz * P.sg_dim[1] + (int)fy) * P.sg_dim[0] + (int)fx;
+        const uint2 e = ((const uint2*)S.sg_cells)[(size_t)P.sg_base[li] + cl];
+        loff = e.x;
+        ln = e.y;
+        lin = ln != 0xffffffffu;
+      }
+      DT_CNT(40);
+      if (!__ballot(active && !lin)) {
+        if (!lin) ln = 0;
+        DT_CNT(41);
+        return bump_list ? occluded_union<true>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt)
+                         : occluded_union<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
+      }
+    }
+#endif
   }
   if (w.bump_wave) return occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
   return occluded_walk<0>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
@@ -1828,13 +1898,6 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
   }
 }
 
-__device__ __forceinline__ unsigned long long wave_sum(uint32_t v)
-{
-  unsigned long long x = v;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
-}
 
 // =====================================================================================
 // render kernel: persistent waves over pixel groups

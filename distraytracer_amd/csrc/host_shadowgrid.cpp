@@ -440,6 +440,16 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       g.cells.push_back((uint32_t)v.size());
     }
     g.n_lights = (int)l + 1;
+    if (getenv("DT_SG_VERBOSE")) {
+      std::vector<char> in_union(nodes.size(), 0);
+      size_t nu = 0, tree_cells = 0;
+      for (int c = 0; c < ncell; ++c) {
+        if ((int)lists[c].size() > DT_SGRID_MAX_LIST) ++tree_cells;
+        for (int32_t x : lists[c]) if (!in_union[x]) { in_union[x] = 1; ++nu; }
+      }
+      fprintf(stderr, "  shadow grid light %zu: union of cell lists %zu of %zu leaves, %zu tree cells\n", l, nu,
+              leaves.size(), tree_cells);
+    }
     if (timing)
       fprintf(stderr, "  shadow grid light %zu: tests %.2f ms (%d threads), lists %.2f ms\n", l, t_tests - t_light, nthr,
               now_ms() - t_tests);
