@@ -48,6 +48,7 @@ struct HScene {
   const int32_t* bparent;   // parent of every reference-tree node
 };
 
+#define DT_N_STAMPS 64   // diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters)
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
        ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15, ST_N = 16 };
 
@@ -229,7 +230,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
     dt_scene_destroy(s);
     return rc;
   }
-  if (hipMalloc((void**)&s->d_stats, sizeof(unsigned long long) * (ST_N + 48)) != hipSuccess ||
+  if (hipMalloc((void**)&s->d_stats, sizeof(unsigned long long) * (ST_N + 1 + DT_N_STAMPS)) != hipSuccess ||
       hipMalloc(&s->d_launch, dt_launch_size()) != hipSuccess || hipEventCreate(&s->ev0) != hipSuccess ||
       hipEventCreate(&s->ev1) != hipSuccess || hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void**)&s->h_launch, dt_launch_size(), hipHostMallocDefault) != hipSuccess ||
@@ -424,7 +425,7 @@ static int enqueue_render(dt_scene* sc, const dtd::DParams& P, const std::vector
   HIPCHK(hipMemcpyAsync(sc->d_launch, sc->h_launch, dt_launch_size(), hipMemcpyHostToDevice, st));
   HIPCHK(hipEventRecord(sc->ev_copy, st));
   sc->copy_pending = true;
-  HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 48), st));
+  HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 1 + DT_N_STAMPS), st));
   HIPCHK(hipEventRecord(sc->ev0, st));
   HIPCHK(dt_launch_trace(sc->d_launch, out_dev, (int)grid, st));
   HIPCHK(hipEventRecord(sc->ev1, st));
@@ -685,8 +686,8 @@ int dt_write_png(const char* filename, int32_t xRes, int32_t yRes, const float* 
 
 extern "C" int dt_debug_counters(const dt_scene* sc, uint64_t* out, int32_t n)
 {
-  if (!sc || !out || n < 0 || n > 47) return fail(DT_E_INVALID, "bad arguments");
-  unsigned long long h[ST_N + 48];
+  if (!sc || !out || n < 0 || n > DT_N_STAMPS) return fail(DT_E_INVALID, "bad arguments");
+  unsigned long long h[ST_N + 1 + DT_N_STAMPS];
   HIPCHK(hipMemcpy(h, sc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
   for (int i = 0; i < n; ++i) out[i] = h[ST_N + 1 + i];
   return DT_OK;

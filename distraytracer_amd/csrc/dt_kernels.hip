@@ -67,6 +67,12 @@ using namespace dtd;
 #ifndef DT_ITEM_BATCH
 #define DT_ITEM_BATCH 0   // wave items per queue atomic; 0: P.item_batch (host: 2 for long runs, else 1)
 #endif
+#ifndef DT_SG_COHERENT
+#define DT_SG_COHERENT 1   // waves within reach of one cell test that cell's list (else: union path)
+#endif
+#ifndef DT_SG_MIXED
+#define DT_SG_MIXED 0      // waves with lanes outside the lists: union for the others, then tree walk
+#endif
 #ifndef DT_LS_CACHE
 #define DT_LS_CACHE 4   // lights whose area-sample pair is kept in LDS between the two light passes
 #endif
@@ -1165,12 +1171,19 @@ __device__ __forceinline__ void shadow_leaf(const DScene& S, const DNodeDev& nd,
     DT_CNT(8);
     DT_CNT(18 + (type & 7));   // shadow prim tests by type (8 -> 18)
     const bool test = hb && !occl && sid != skip_shape;
+#ifdef DT_STAMPS
+    const unsigned long long occ_before = __ballot(occl);
+#endif
     if (test) {
       DT_WORK(cnt.prim++);
 #ifndef DT_ABL_NOPRIM_SHADOW
       if (shape_shadow(type, flags, cas(S.geom) + off, sn, sstart, t_max, shift)) occl = true;
 #endif
     }
+#ifdef DT_STAMPS
+    cnt.ph[47 + (type & 7)] += __popcll(__ballot(test));
+    cnt.ph[55 + (type & 7)] += __popcll(__ballot(occl) & ~occ_before);
+#endif
   }
   DT_T(q1);
   DT_ACC(32, q0, q1);
@@ -1259,12 +1272,18 @@ __device__ bool occluded_list(const DScene& S, const Walk& w, bool active, V3 bs
   return occl;
 }
 
-// wave minimum of a per-lane int (DPP/swizzle butterfly; every lane gets the result)
-__device__ __forceinline__ int wave_min_i32(int v)
+// wave minimum of a per-lane int, returned wave-uniform: DPP within rows of 16 (quad perms, half
+// mirror, mirror: no LDS round trips), then the four row minima through readlane on the scalar unit.
+// Every lane must be enabled in exec (the callers run at wave-uniform control flow).
+__device__ __forceinline__ int wave_min_u(int v)
 {
-#pragma unroll
-  for (int o = 1; o < DT_WAVE; o <<= 1) v = min(v, __shfl_xor(v, o, DT_WAVE));
-  return v;
+  v = min(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));    // quad_perm [1,0,3,2]
+  v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
+  v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));   // row_half_mirror
+  v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));   // row_mirror
+  const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+  const int c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  return min(min(a, b), min(c, d));
 }
 
 // Scattered waves (lanes in different grid cells): each lane's own cell list holds every leaf that
@@ -1279,9 +1298,11 @@ __device__ bool occluded_union(const DScene& S, const Walk& w, bool active, V3 b
   bool occl = false;
   const float tcull = shadow_tcull(t_max);
   uint32_t k = 0;
+  // head: the lane's next leaf; nxt: the one after it, loaded an iteration ahead
   int head = (active && n > 0) ? S.sg_list[off] : INT_MAX;
+  int nxt = (active && n > 1) ? S.sg_list[off + 1] : INT_MAX;
   while (true) {
-    const int m = uni(wave_min_i32(occl ? INT_MAX : head));
+    const int m = wave_min_u(occl ? INT_MAX : head);
     if (m == INT_MAX) break;
     const DNodeDev nd = cas(S.nodes)[m];
     const bool hb = active & !occl &
@@ -1290,7 +1311,8 @@ __device__ bool occluded_union(const DScene& S, const Walk& w, bool active, V3 b
     if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, shift, cnt);
     if (head == m) {
       ++k;
-      head = k < n ? S.sg_list[off + k] : INT_MAX;
+      head = nxt;
+      nxt = k + 1 < n ? S.sg_list[off + k + 1] : INT_MAX;
     }
   }
   return occl;
@@ -1324,6 +1346,7 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   // walk); a wave with a lane outside the grid or in a cell whose list is too long walks the tree.
   // Measured slower for scattered waves: per-lane list walks with a per-lane shape switch (C3 1725
   // vs 1932, C4 843 vs 936 Mpixel-samples/s), the lists of two cells in turn.
+  bool occ_union = false;   // DT_SG_MIXED: lanes answered by the union walk
   if (li < P.sg_n && P.sg_base[li] >= 0) {
     const unsigned long long am = __ballot(active);
     if (!am) return false;
@@ -1339,7 +1362,7 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
     const bool near = (x >= x0 - r) & (x <= x0 + 1.0f + r) & (y >= y0 - r) & (y <= y0 + 1.0f + r) &
                       (z >= z0 - r) & (z <= z0 + 1.0f + r);
     DT_CNT(inside ? 36 : 38);
-    if (inside && !__ballot(active & !near)) {
+    if (DT_SG_COHERENT && inside && !__ballot(active & !near)) {
       const int c0 = ((int)z0 * P.sg_dim[1] + (int)y0) * P.sg_dim[0] + (int)x0;
       const DT_CAS uint32_t* e = cas(S.sg_cells) + 2 * (size_t)(P.sg_base[li] + c0);
       const uint32_t off = e[0], n = e[1];
@@ -1364,17 +1387,31 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
         lin = ln != 0xffffffffu;
       }
       DT_CNT(40);
-      if (!__ballot(active && !lin)) {
-        if (!lin) ln = 0;
+      if (!lin) ln = 0;
+      const unsigned long long out_lanes = __ballot(active && !lin);
+#if DT_SG_MIXED
+      // lanes with a list take the union; the rest (outside the grid, or in a cell whose list is
+      // too long) walk the tree afterwards, unless the union already occluded them all
+      if (__ballot(active && lin)) {
+        DT_CNT(41);
+        const bool o = bump_list ? occluded_union<true>(S, w, active && lin, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt)
+                                 : occluded_union<false>(S, w, active && lin, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
+        if (!out_lanes) return o;
+        active = active && !lin;
+        occ_union = o;
+      }
+#else
+      if (!out_lanes) {
         DT_CNT(41);
         return bump_list ? occluded_union<true>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt)
                          : occluded_union<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
       }
+#endif
     }
 #endif
   }
-  if (w.bump_wave) return occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
-  return occluded_walk<0>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+  if (w.bump_wave) return occ_union | occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+  return occ_union | occluded_walk<0>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 }
 
 // =====================================================================================
@@ -1402,7 +1439,7 @@ struct Counters {
   uint32_t box, prim;
   uint32_t wnodes;                   // wave-level
 #ifdef DT_STAMPS
-  unsigned long long ph[47];   // diagnostic build only: cycles per phase, event counts (wave-uniform)
+  unsigned long long ph[64];   // diagnostic build only: cycles per phase, event counts (wave-uniform)
 #endif
 };
 
@@ -1579,7 +1616,13 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     DT_T(t1);
     DT_ACC(0, t0, t1);
     HitRec h;
+#ifdef DT_STAMPS
+    const unsigned long long v_before = cnt.ph[26];
+#endif
     bool any = closest_hit(S, P, have, ray, eye, shift, h, cnt);
+#ifdef DT_STAMPS
+    if (__ballot(is_root)) { cnt.ph[46] += cnt.ph[26] - v_before; cnt.ph[39] += 1; }
+#endif
     DT_T(t2);
     DT_ACC(1, t1, t2);
     any = any && have && h.shape >= 0;
@@ -1984,7 +2027,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   Counters cnt;
   cnt.rays = 0; cnt.shadow = 0; cnt.tex = 0; cnt.box = 0; cnt.prim = 0; cnt.wnodes = 0;
 #ifdef DT_STAMPS
-  for (int k = 0; k < 47; ++k) cnt.ph[k] = 0;
+  for (int k = 0; k < 64; ++k) cnt.ph[k] = 0;
 #endif
 
   int64_t item = 0, batch_end = 0;
@@ -2130,7 +2173,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       atomicAdd(S.stats + ST_PRIM, pr);
       atomicAdd(S.stats + ST_WNODES, (unsigned long long)cnt.wnodes);
 #ifdef DT_STAMPS
-      for (int k = 0; k < 47; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);
+      for (int k = 0; k < 64; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);
 #endif
       if (sky_px) atomicAdd(S.stats + ST_SKY, sky_px);
       atomicAdd(S.stats + ST_RAYS, r);

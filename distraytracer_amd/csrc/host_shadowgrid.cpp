@@ -270,6 +270,9 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   // 
   const char* so = getenv("DT_SG_ORDER");
   const bool order_lists = so && atoi(so) != 0;
+  // DT_SG_MAX_LIST: cells with longer lists walk the tree instead (default DT_SGRID_MAX_LIST)
+  const char* mls = getenv("DT_SG_MAX_LIST");
+  const int max_list = mls && atoi(mls) > 0 ? atoi(mls) : DT_SGRID_MAX_LIST;
   int blk_x = 8, blk_y = 4;
   if (!sg_parse_block(getenv("DT_SG_BLOCK"), blk_x, blk_y))
     fprintf(stderr, "dt: DT_SG_BLOCK='%s' not understood (use 0 or XxY with X, Y >= 1): default 8x4\n",
@@ -397,7 +400,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
         const int y = row % g.dim[1], z = row / g.dim[1];
         for (int x = 0; x < g.dim[0]; ++x) {
           std::vector<int32_t>& v = lists[(size_t)row * g.dim[0] + x];
-          if (v.size() < 2 || (int)v.size() > DT_SGRID_MAX_LIST) continue;
+          if (v.size() < 2 || (int)v.size() > max_list) continue;
           const int ci[3] = {x, y, z};
           double p[3];
           for (int a = 0; a < 3; ++a) p[a] = lo[a] + (ci[a] + 0.5) * hh[a];
@@ -422,7 +425,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
     g.base[l] = (int32_t)g.cells.size() / 2;
     for (int c = 0; c < ncell; ++c) {
       std::vector<int32_t>& v = lists[c];
-      if ((int)v.size() > DT_SGRID_MAX_LIST) {   // the tree walk is cheaper for long lists
+      if ((int)v.size() > max_list) {   // the tree walk is cheaper for long lists
         g.cells.push_back(0);
         g.cells.push_back(0xffffffffu);
         continue;
@@ -444,7 +447,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       std::vector<char> in_union(nodes.size(), 0);
       size_t nu = 0, tree_cells = 0;
       for (int c = 0; c < ncell; ++c) {
-        if ((int)lists[c].size() > DT_SGRID_MAX_LIST) ++tree_cells;
+        if ((int)lists[c].size() > max_list) ++tree_cells;
         for (int32_t x : lists[c]) if (!in_union[x]) { in_union[x] = 1; ++nu; }
       }
       fprintf(stderr, "  shadow grid light %zu: union of cell lists %zu of %zu leaves, %zu tree cells\n", l, nu,

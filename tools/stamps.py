@@ -26,8 +26,8 @@ def main():
     s = dt.Scene(b, g)
     out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
     st = dt.render(s, g, frame, out)
-    arr = (ctypes.c_uint64 * 47)()
-    dt.check(dt.lib.dt_debug_counters(s.handle, arr, 47))
+    arr = (ctypes.c_uint64 * 64)()
+    dt.check(dt.lib.dt_debug_counters(s.handle, arr, 64))
     tot = arr[5] + arr[6]
     print("kernel ms %.2f" % st.kernel_ms)
     for i, n in enumerate(NAMES[:7]):
@@ -39,7 +39,11 @@ def main():
              0: "checkercyl"}
     print("closest-hit prim tests per item:", {names[t]: round(arr[10 + t] / items, 2) for t in range(8) if arr[10 + t]})
     print("shadow prim tests per item:", {names[t]: round(arr[18 + t] / items, 2) for t in range(8) if arr[18 + t]})
+    print("shadow prim tests, lanes tested per item / hit fraction:",
+          {names[t]: (round(arr[47 + t] / items, 1), round(arr[55 + t] / max(arr[47 + t], 1), 3)) for t in range(8) if arr[47 + t]})
     print("node visits per item: closest-hit %.1f  shadow %.1f" % (arr[26] / items, arr[27] / items))
+    print("closest-hit root walks per item %.2f with %.1f node visits per walk; other walks %.1f visits per walk"
+          % (arr[39] / items, arr[46] / max(arr[39], 1), (arr[26] - arr[46]) / max(arr[7] - arr[39], 1)))
     print("cycles in shadow leaf/prim blocks %.2f%%, closest-hit leaf/prim blocks %.2f%%"
           % (100.0 * arr[32] / max(tot, 1), 100.0 * arr[33] / max(tot, 1)))
     print("shadow grid per item: list tests %.1f, list walks %.2f, cell lookups inside %.2f / outside %.2f, "
