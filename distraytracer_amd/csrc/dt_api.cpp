@@ -46,6 +46,8 @@ struct HScene {
   unsigned long long* queue;
   const void* bnodes;       // motion-blur bump tree (host_fasttree.cpp)
   const int32_t* bparent;   // parent of every reference-tree node
+  const uint32_t* pl_cells; // primary-ray candidate lists (host_primlists.cpp)
+  const uint32_t* pl_list;
 };
 
 #define DT_N_STAMPS 64   // diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters)
@@ -124,6 +126,13 @@ struct dt_scene {
   float* h_zs = nullptr;          // pinned staging for the cloud z sequence
   bool copy_pending = false;
   bool timed = false;
+  // primary-ray candidate lists, rebuilt when the camera / resolution changes (host_primlists.cpp)
+  std::vector<dtd::DNodeDev> fnodes_host;
+  std::vector<double> pl_key;
+  PrimLists pl;
+  bool pl_ok = false;
+  void* d_pl_cells = nullptr;
+  void* d_pl_list = nullptr;
   dtd::DParams last;
 };
 
@@ -219,6 +228,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
   s->ftree_mode = acc.ftree_mode;
   s->boxes_ordered = acc.boxes_ordered;
   s->sg = std::move(acc.sg);
+  s->fnodes_host = acc.fnodes;
   if ((rc = upload(s->sg.cells, &s->d_sg_cells)) || (rc = upload(s->sg.list, &s->d_sg_list))) {
     dt_scene_destroy(s);
     return rc;
@@ -246,7 +256,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
 void dt_scene_destroy(dt_scene* s)
 {
   if (!s) return;
-  void* bufs[] = {s->d_nodes, s->d_fnodes, s->d_bnodes, s->d_bparent, s->d_sg_cells, s->d_sg_list, s->d_leaf, s->d_hdr, s->d_geom, s->d_mat, s->d_lights, s->d_tex, s->d_zs,
+  void* bufs[] = {s->d_pl_cells, s->d_pl_list, s->d_nodes, s->d_fnodes, s->d_bnodes, s->d_bparent, s->d_sg_cells, s->d_sg_list, s->d_leaf, s->d_hdr, s->d_geom, s->d_mat, s->d_lights, s->d_tex, s->d_zs,
                   s->d_stats, s->d_launch};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -378,9 +388,47 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   return DT_OK;
 }
 
-static int enqueue_render(dt_scene* sc, const dtd::DParams& P, const std::vector<float>& zs, float* out_dev,
+// Primary-ray candidate lists for P's camera (DT_PRIM_LISTS=0 disables them; DT_PL_BLOCK: pixels
+// per block side, default 8). Rebuilt only when the camera or resolution changes; the device copy
+// is replaced after the device has drained, since earlier launches may still read it.
+static int update_primary_lists(dt_scene* sc, dtd::DParams& P)
+{
+  P.pl_block = P.pl_nbx = P.pl_nby = 0;
+  const char* e = getenv("DT_PRIM_LISTS");
+  if ((e && e[0] == '0') || sc->n_fnodes <= 0 || !(sc->ftree_mode & 1)) return DT_OK;
+  const char* b = getenv("DT_PL_BLOCK");
+  const int B = b && atoi(b) > 0 ? atoi(b) : 8;
+  std::vector<double> key = {(double)B, (double)P.xRes, (double)P.yRes, (double)P.l, (double)P.r, (double)P.t,
+                             (double)P.b, (double)P.focal_length, (double)P.near_plane, (double)P.aperture};
+  for (int k = 0; k < 3; ++k) key.insert(key.end(), {P.eye[k], P.X[k], P.Y[k], P.Z[k]});
+  if (key != sc->pl_key) {
+    HIPCHK(hipDeviceSynchronize());
+    sc->pl_key = key;
+    sc->pl_ok = build_primary_lists(sc->fnodes_host, sc->n_fnodes, P, B, sc->pl);
+    if (sc->d_pl_cells) (void)hipFree(sc->d_pl_cells);
+    if (sc->d_pl_list) (void)hipFree(sc->d_pl_list);
+    sc->d_pl_cells = sc->d_pl_list = nullptr;
+    if (sc->pl_ok) {
+      int rc;
+      if ((rc = upload(sc->pl.cells, &sc->d_pl_cells)) || (rc = upload(sc->pl.list, &sc->d_pl_list))) {
+        sc->pl_ok = false;
+        sc->pl_key.clear();
+        return rc;
+      }
+    }
+  }
+  if (sc->pl_ok) {
+    P.pl_block = sc->pl.block;
+    P.pl_nbx = sc->pl.nbx;
+    P.pl_nby = sc->pl.nby;
+  }
+  return DT_OK;
+}
+
+static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>& zs, float* out_dev,
                           hipStream_t st)
 {
+  if (int rc = update_primary_lists(sc, P)) return rc;
   // Fully asynchronous: the launch record and z table go through pinned staging that is
   // only rewritten after the previous call's copies have executed (ev_copy); the device
   // copies themselves are stream-ordered after any earlier kernel that reads them.
@@ -410,6 +458,8 @@ static int enqueue_render(dt_scene* sc, const dtd::DParams& P, const std::vector
   hs.cloud_z = (const float*)sc->d_zs;
   hs.stats = sc->d_stats;
   hs.queue = sc->d_stats + ST_N;
+  hs.pl_cells = (const uint32_t*)sc->d_pl_cells;
+  hs.pl_list = (const uint32_t*)sc->d_pl_list;
   static int resident = 0;
   if (!resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
   int64_t grid = P.n_items < resident ? P.n_items : resident;

@@ -118,6 +118,8 @@ struct DScene {
   unsigned long long* queue;
   const DNodeDev* bnodes;   // bump tree for motion-blur passes (host_fasttree.cpp; leaf skip = reference index)
   const int32_t* bparent;   // parent of every reference node (-1: root)
+  const uint32_t* pl_cells; // primary-ray candidate lists (host_primlists.cpp): (first, count) per pixel block
+  const uint32_t* pl_list;  // (fast-tree node, float bits of t_near) per entry
 };
 
 // pow(x, n) for the integer exponents the reference writes as pow(x, 2.0) etc. pow(x, 1) is x
@@ -1140,15 +1142,75 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
   return any;
 }
 
+// Closest hit of primary rays over their pixel block's candidate leaves (host_primlists.cpp), in
+// order of the smallest ray parameter each leaf's box can be reached at: once every lane's best hit
+// lies before the next entry, no later leaf can change a result. Same box filter, shape tests and
+// tie rule (reference rank) as the fast-tree walk.
+template <class CNT>
+__device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams& P, const Walk& w, bool active, V3 ray,
+                                                  V3 org, HitRec& h, uint32_t off, uint32_t n, CNT& cnt)
+{
+  float t_dist = FLT_MAX;
+  bool any = false;
+  h.t_min = FLT_MAX;
+  h.shape = -1;
+  h.rank = 0x7fffffff;
+  h.edge = 0;
+  h.inside = 0;
+  h.ccol = -1;
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t node = __builtin_amdgcn_readfirstlane(cas(S.pl_list)[2 * (size_t)(off + k)]);
+    const float tn = __uint_as_float(__builtin_amdgcn_readfirstlane(cas(S.pl_list)[2 * (size_t)(off + k) + 1]));
+    if (!__ballot(active && !(h.t_min < tn))) break;
+    const DNodeDev nd = cas(S.fnodes)[node];
+    const float tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
+    bool hb = active & node_hit<false>(w, nd, 0.0f, org, tcull);
+    DT_WORK(cnt.wnodes++; cnt.box += active);
+    DT_CNT(26);
+    if (__ballot(hb)) {
+      const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
+      const int rank = (int)(nd.meta >> 16);
+      for (int q = 0; q < nq; ++q) {
+        int sid, type, off2;
+        uint32_t flags;
+        leaf_shape(S, nd, q, sid, type, flags, off2);
+        DT_CNT(8);
+        DT_CNT(10 + (type & 7));
+        if (hb) {
+          DT_WORK(cnt.prim++);
+          int ins = 0, cc = -1;
+          if (shape_hit(S, sid, type, flags, cas(S.geom) + off2, ray, org, 0.0f, t_dist, ins, cc, h.edge)) {
+            any = true;
+            if (t_dist < h.t_min || (t_dist == h.t_min && rank < h.rank)) {
+              h.rank = rank;
+              h.shape = sid;
+              h.inside = ins;
+              h.t_min = t_dist;
+              h.ccol = cc;
+            }
+          }
+        }
+      }
+    }
+  }
+  return any;
+}
+
 template <class CNT>
 __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 ray, V3 org, float shift,
-                                            HitRec& h, CNT& cnt)
+                                            HitRec& h, CNT& cnt, int pblock = -1)
 {
   const Walk w = make_walk(P, active, ray, org, shift);
   if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift)))
     return closest_hit_walk<1>(S, P, w, active, ray, org, shift, h, cnt);
-  const bool any = w.bump_wave ? closest_hit_walk<2>(S, P, w, active, ray, org, shift, h, cnt)
-                               : closest_hit_walk<0>(S, P, w, active, ray, org, shift, h, cnt);
+  bool any;
+  if (pblock >= 0 && !w.bump_wave) {
+    const uint32_t off = cas(S.pl_cells)[2 * pblock], n = cas(S.pl_cells)[2 * pblock + 1];
+    any = closest_hit_plist(S, P, w, active, ray, org, h, off, n, cnt);
+  } else {
+    any = w.bump_wave ? closest_hit_walk<2>(S, P, w, active, ray, org, shift, h, cnt)
+                      : closest_hit_walk<0>(S, P, w, active, ray, org, shift, h, cnt);
+  }
   // an edge-on checkerboard hit keeps the previous test's t (Q16): only the reference order
   // reproduces it, so with the alternative trees such waves (never seen in practice) repeat the
   // walk on the reference tree
@@ -1619,7 +1681,16 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
 #ifdef DT_STAMPS
     const unsigned long long v_before = cnt.ph[26];
 #endif
-    bool any = closest_hit(S, P, have, ray, eye, shift, h, cnt);
+    // primary rays of a pass without a shift: the pixel block's candidate list, when the wave's
+    // pixels share one block (host_primlists.cpp)
+    int pblock = -1;
+    if (P.pl_block > 0 && __ballot(is_root) && !__ballot(have && shift != 0.0f) && P.n_fnodes > 0 && (P.ftree_mode & 1)) {
+      const int px = (int)(c.rng.pixel % (uint32_t)P.xRes), py = (int)(c.rng.pixel / (uint32_t)P.xRes);
+      const int blk = (py / P.pl_block) * P.pl_nbx + px / P.pl_block;
+      const int b0 = uni(blk);
+      if (!__ballot(have && blk != b0)) pblock = b0;
+    }
+    bool any = closest_hit(S, P, have, ray, eye, shift, h, cnt, pblock);
 #ifdef DT_STAMPS
     if (__ballot(is_root)) { cnt.ph[46] += cnt.ph[26] - v_before; cnt.ph[39] += 1; }
 #endif

@@ -77,6 +77,16 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a,
 uint64_t sg_hash(const ShadowGrid& sg, bool contents_only);
 uint64_t nodes_hash(const std::vector<dtd::DNodeDev>& v);
 
+// host_primlists.cpp: per pixel-block candidate leaves (fast-tree node indices, sorted by the
+// smallest ray parameter they can be reached at) for the primary rays' closest hit
+struct PrimLists {
+  int block = 0, nbx = 0, nby = 0;
+  std::vector<uint32_t> cells;   // (first entry, count) per block
+  std::vector<uint32_t> list;    // (fast-tree node, float bits of t_near) per entry
+};
+bool build_primary_lists(const std::vector<dtd::DNodeDev>& fnodes, int n_fnodes, const dtd::DParams& P, int B,
+                         PrimLists& out);
+
 // camera / params (host_flatten.cpp)
 int fill_params(const dt_globals& g, int frame, const dt_tiles* tiles, dtd::DParams& P, std::string& err);
 int fill_sky_params(const dt_globals& g, float frame, const dt_tiles* tiles, dtd::DParams& P, std::string& err);

@@ -259,6 +259,36 @@ def test_shadow_grid_matches_tree_walks(cuda, monkeypatch):
         assert np.array_equal(img, ref_img), env
 
 
+PL_CASES = [  # (name, builder, frame, models, W, H, spp, depth, window)
+    ("c3", "final", 240, 0, 1920, 1080, 64, 8, (880, 480, 1008, 560)),
+    ("c4-models", "final", 240, 1, 1920, 1080, 16, 3, (1200, 500, 1296, 580)),
+    ("c1-dof", "spheres", 0, 0, 256, 256, 16, 2, (64, 64, 192, 192)),
+    ("c5-tunnel", "final", 1200, 0, 320, 180, 16, 3, (96, 40, 224, 136)),
+    ("c2-full", "final", 240, 0, 200, 150, 4, 4, (0, 0, 200, 150)),
+]
+
+
+@pytest.mark.parametrize("case", PL_CASES, ids=[c[0] for c in PL_CASES])
+def test_primary_lists_match_tree_walks(cuda, monkeypatch, case):
+    """Primary rays over their pixel block's candidate leaves (host_primlists.cpp: camera-space
+    frustum of the block's DoF rays, leaves sorted by reach, early exit) must give the image of
+    fast-tree walks bit for bit, for any block size (a ragged last block included)."""
+    name, builder, frame, models, W, H, spp, depth, win = case
+    g = dt.globals_default()
+    g.use_model = models
+    built = dt.build_scene(builder, frame, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = W, H, spp, depth
+    tile = dt.tiles(x0=win[0], y0=win[1], x1=win[2], y1=win[3])
+    monkeypatch.setenv("DT_PRIM_LISTS", "0")
+    ref_img, ref_st = _render_gpu(built, g, frame, tile)
+    monkeypatch.delenv("DT_PRIM_LISTS")
+    for blk in ("8", "3", "16"):
+        monkeypatch.setenv("DT_PL_BLOCK", blk)
+        img, st = _render_gpu(built, g, frame, tile)
+        assert st.rays == ref_st.rays and st.shadow_rays == ref_st.shadow_rays, blk
+        assert np.array_equal(img, ref_img), blk
+
+
 @pytest.mark.parametrize("n", [150, 210])
 def test_bump_tree_matches_reference_walks(cuda, monkeypatch, n):
     """Motion-blur passes on the bump tree (host_fasttree.cpp: padded leaves, exact per-leaf
