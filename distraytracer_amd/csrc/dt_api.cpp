@@ -50,7 +50,8 @@ struct HScene {
   const uint32_t* pl_list;
 };
 
-#define DT_N_STAMPS 64   // diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters)
+#define DT_N_STAMPS (64 + 3 * 8 * 256)   // diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters):
+                                         // phases, then (waves, lanes, hits) per (light, shape) shadow test
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
        ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15, ST_N = 16 };
 
@@ -737,8 +738,8 @@ int dt_write_png(const char* filename, int32_t xRes, int32_t yRes, const float* 
 extern "C" int dt_debug_counters(const dt_scene* sc, uint64_t* out, int32_t n)
 {
   if (!sc || !out || n < 0 || n > DT_N_STAMPS) return fail(DT_E_INVALID, "bad arguments");
-  unsigned long long h[ST_N + 1 + DT_N_STAMPS];
-  HIPCHK(hipMemcpy(h, sc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  std::vector<unsigned long long> h(ST_N + 1 + DT_N_STAMPS);
+  HIPCHK(hipMemcpy(h.data(), sc->d_stats, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
   for (int i = 0; i < n; ++i) out[i] = h[ST_N + 1 + i];
   return DT_OK;
 }

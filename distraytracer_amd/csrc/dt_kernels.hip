@@ -1245,6 +1245,12 @@ __device__ __forceinline__ void shadow_leaf(const DScene& S, const DNodeDev& nd,
 #ifdef DT_STAMPS
     cnt.ph[47 + (type & 7)] += __popcll(__ballot(test));
     cnt.ph[55 + (type & 7)] += __popcll(__ballot(occl) & ~occ_before);
+    if ((threadIdx.x & 63) == 0 && sid < 256 && cnt.cur_li < 8) {   // per (light, shape): waves, lanes, hits
+      unsigned long long* h = S.stats + ST_N + 1 + 64 + 3 * (cnt.cur_li * 256 + sid);
+      atomicAdd(h, 1ull);
+      atomicAdd(h + 1, (unsigned long long)__popcll(__ballot(test)));
+      atomicAdd(h + 2, (unsigned long long)__popcll(__ballot(occl) & ~occ_before));
+    }
 #endif
   }
   DT_T(q1);
@@ -1502,6 +1508,7 @@ struct Counters {
   uint32_t wnodes;                   // wave-level
 #ifdef DT_STAMPS
   unsigned long long ph[64];   // diagnostic build only: cycles per phase, event counts (wave-uniform)
+  int cur_li;                  // light of the current shadow test (per-shape histogram)
 #endif
 };
 
@@ -1885,6 +1892,9 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           cnt.shadow++;
         }
         DT_T(t4);
+#ifdef DT_STAMPS
+        cnt.cur_li = li;
+#endif
         bool occl = occluded(S, P, walk, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
                              t_max, L.shape_index, li, shift, cnt);
         DT_T(t5);
@@ -2099,6 +2109,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   cnt.rays = 0; cnt.shadow = 0; cnt.tex = 0; cnt.box = 0; cnt.prim = 0; cnt.wnodes = 0;
 #ifdef DT_STAMPS
   for (int k = 0; k < 64; ++k) cnt.ph[k] = 0;
+  cnt.cur_li = 0;
 #endif
 
   int64_t item = 0, batch_end = 0;

@@ -26,8 +26,9 @@ def main():
     s = dt.Scene(b, g)
     out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
     st = dt.render(s, g, frame, out)
-    arr = (ctypes.c_uint64 * 64)()
-    dt.check(dt.lib.dt_debug_counters(s.handle, arr, 64))
+    NS = 64 + 3 * 8 * 256
+    arr = (ctypes.c_uint64 * NS)()
+    dt.check(dt.lib.dt_debug_counters(s.handle, arr, NS))
     tot = arr[5] + arr[6]
     print("kernel ms %.2f" % st.kernel_ms)
     for i, n in enumerate(NAMES[:7]):
@@ -51,6 +52,26 @@ def main():
     print("scattered shadow waves per item %.2f, union walks %.2f" % (arr[40] / items, arr[41] / items))
     print("shadow walks per item: all occluded %.2f (%.1f visits/walk), none occluded %.2f (%.1f/walk), total %.2f"
           % (arr[29] / items, arr[28] / max(arr[29], 1), arr[31] / items, arr[30] / max(arr[31], 1), arr[9] / items))
+    # per (light, shape) shadow tests: wave-level tests per item, lanes per test, lane hit fraction
+    d = b.desc
+    rows = []
+    for li in range(8):
+        for sid in range(256):
+            o = 64 + 3 * (li * 256 + sid)
+            if arr[o]:
+                rows.append((arr[o], li, sid, arr[o + 1], arr[o + 2]))
+    rows.sort(reverse=True)
+    print("top shadow tests (light, shape, type): waves/item lanes/test hit-frac  v0 v2")
+    for w, li, sid, ln, hi in rows[:30]:
+        sh = d.shapes[sid] if sid < d.n_shapes else None
+        ty = names.get(sh.type & 7, sh.type) if sh else "?"
+        v0 = tuple(round(sh.v[0][k], 2) for k in range(3)) if sh else ()
+        v2 = tuple(round(sh.v[2][k], 2) for k in range(3)) if sh else ()
+        print("  L%d s%-3d %-11s %6.3f %5.1f %6.3f  %s %s" % (li, sid, ty, w / items, ln / w, hi / max(ln, 1), v0, v2))
+    for li in range(d.n_lights):
+        L = d.lights[li]
+        print("  light %d type %d shape %d center %s A %s" % (li, L.type, L.shape_index,
+              tuple(round(L.center[k], 2) for k in range(3)), tuple(round(L.A[k], 2) for k in range(3))))
 
 
 if __name__ == "__main__":
