@@ -1245,11 +1245,14 @@ __device__ __forceinline__ void shadow_leaf(const DScene& S, const DNodeDev& nd,
 #ifdef DT_STAMPS
     cnt.ph[47 + (type & 7)] += __popcll(__ballot(test));
     cnt.ph[55 + (type & 7)] += __popcll(__ballot(occl) & ~occ_before);
-    if ((threadIdx.x & 63) == 0 && sid < 256 && cnt.cur_li < 8) {   // per (light, shape): waves, lanes, hits
-      unsigned long long* h = S.stats + ST_N + 1 + 64 + 3 * (cnt.cur_li * 256 + sid);
-      atomicAdd(h, 1ull);
-      atomicAdd(h + 1, (unsigned long long)__popcll(__ballot(test)));
-      atomicAdd(h + 2, (unsigned long long)__popcll(__ballot(occl) & ~occ_before));
+    {   // per (light, shape): waves, lanes, hits (ballots taken by the whole wave, added by lane 0)
+      const unsigned long long bt = __ballot(test), bo = __ballot(occl) & ~occ_before;
+      if ((threadIdx.x & 63) == 0 && sid < 254 && cnt.cur_li < 8) {
+        unsigned long long* h = S.stats + ST_N + 1 + 64 + 3 * (cnt.cur_li * 256 + sid);
+        atomicAdd(h, 1ull);
+        atomicAdd(h + 1, (unsigned long long)__popcll(bt));
+        atomicAdd(h + 2, (unsigned long long)__popcll(bo));
+      }
     }
 #endif
   }
@@ -1899,6 +1902,18 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
                              t_max, L.shape_index, li, shift, cnt);
         DT_T(t5);
         DT_ACC(3, t4, t5);
+#ifdef DT_STAMPS
+        {   // per light: (waves, active lanes, occluded lanes), (cycles)
+          const unsigned long long bw = __ballot(walk), bo = __ballot(walk && occl);
+          if ((threadIdx.x & 63) == 0 && li < 8) {
+            unsigned long long* h = S.stats + ST_N + 1 + 64 + 3 * (li * 256 + 255);
+            atomicAdd(h, 1ull);
+            atomicAdd(h + 1, (unsigned long long)__popcll(bw));
+            atomicAdd(h + 2, (unsigned long long)__popcll(bo));
+            atomicAdd(h - 3, (unsigned long long)(t5 - t4));
+          }
+        }
+#endif
         if (walk && !occl) vis |= 1u << li;
       }
       asm volatile("" ::: "memory");

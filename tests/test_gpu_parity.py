@@ -247,9 +247,9 @@ def test_shadow_grid_matches_tree_walks(cuda, monkeypatch):
     # themselves) and the likely-occluder list order (any-hit: the image must not change)
     variants = [{"DT_SG_CELLS": "32768", "DT_SG_REACH": "0.5"}, {"DT_SG_CELLS": "4096", "DT_SG_REACH": "2"}]
     variants += [{"DT_SG_BLOCK": b, "DT_SG_ORDER": o} for b in ("0", "4x2", "32x8") for o in ("0", "1")]
-    variants += [{"DT_SG_ORDER": "1"}]
+    variants += [{"DT_SG_ORDER": "1"}, {"DT_SG_HULL": "0"}, {"DT_SG_HULL": "2"}]
     for env in variants:
-        for k in ("DT_SG_CELLS", "DT_SG_REACH", "DT_SG_BLOCK", "DT_SG_ORDER"):
+        for k in ("DT_SG_CELLS", "DT_SG_REACH", "DT_SG_BLOCK", "DT_SG_ORDER", "DT_SG_HULL"):
             monkeypatch.delenv(k, raising=False)
         monkeypatch.setenv("DT_SHADOW_GRID", "1")
         for k, v in env.items():
@@ -257,6 +257,28 @@ def test_shadow_grid_matches_tree_walks(cuda, monkeypatch):
         img, st = _render_gpu(built, g, 240, tile)
         assert st.shadow_rays == ref_st.shadow_rays, env
         assert np.array_equal(img, ref_img), env
+
+
+@pytest.mark.parametrize("frame", [1200, 1680])
+def test_shadow_grid_hull_culling_tunnel(cuda, monkeypatch, frame):
+    """Hull culling (host_shadowgrid.cpp) drops the tunnel's slanted panels from the cells whose
+    segments to the light cannot reach them: C5 tunnel windows (ads in motion, blur passes on the
+    padded lists) must match tree walks bit for bit with it off, on blocks, and on blocks + cells."""
+    g = dt.globals_default()
+    g.use_model = 0
+    built = dt.build_scene("final", frame, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = 480, 270, 16, 10
+    tile = dt.tiles(x0=160, y0=80, x1=320, y1=176)
+    for k in ("DT_SG_CELLS", "DT_SG_REACH", "DT_SG_BLOCK", "DT_SG_ORDER", "DT_SG_HULL"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("DT_SHADOW_GRID", "0")
+    ref_img, ref_st = _render_gpu(built, g, frame, tile)
+    monkeypatch.setenv("DT_SHADOW_GRID", "1")
+    for mode in ("0", "1", "2"):
+        monkeypatch.setenv("DT_SG_HULL", mode)
+        img, st = _render_gpu(built, g, frame, tile)
+        assert st.shadow_rays == ref_st.shadow_rays, mode
+        assert np.array_equal(img, ref_img), mode
 
 
 PL_CASES = [  # (name, builder, frame, models, W, H, spp, depth, window)

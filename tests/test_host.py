@@ -156,7 +156,7 @@ def test_oracle_sky_image_cloud_anchor():
 # ---- acceleration structures built on the host (dt_accel_info_build) ------------------------
 
 def _accel(name, frame, models, env, monkeypatch):
-    for k in ("DT_SG_BLOCK", "DT_SG_ORDER"):
+    for k in ("DT_SG_BLOCK", "DT_SG_ORDER", "DT_SG_HULL"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -170,20 +170,36 @@ def _accel(name, frame, models, env, monkeypatch):
 ACCEL_SCENES = [("c3", 240, 0), ("c4", 240, 1), ("c5-tunnel", 1200, 0)]
 
 
+@pytest.mark.parametrize("hull", ["0", "2"])
 @pytest.mark.parametrize("name,frame,models", ACCEL_SCENES, ids=[s[0] for s in ACCEL_SCENES])
-def test_shadow_grid_block_tests_give_identical_lists(name, frame, models, monkeypatch):
+def test_shadow_grid_block_tests_give_identical_lists(name, frame, models, hull, monkeypatch):
     """The per-block (leaf, cell) rejection (host_shadowgrid.cpp) is exact only while the swept
-    test and the plane separation stay monotone in the cell box: every block size must give the
-    per-cell build's lists bit for bit (cells, counts and pool, in storage order)."""
-    base = _accel(name, frame, models, {"DT_SG_BLOCK": "0"}, monkeypatch)
+    test, the plane separation and the hull separation stay monotone in the cell box: with hull
+    culling off (0) or on every cell (2), every block size must give the per-cell build's lists
+    bit for bit (cells, counts and pool, in storage order)."""
+    base = _accel(name, frame, models, {"DT_SG_BLOCK": "0", "DT_SG_HULL": hull}, monkeypatch)
     assert base["sg_lights"] > 0 and base["sg_list_entries"] > 0
     for blk in ("4x2", "8x4", "32x8", "1x1"):
-        got = _accel(name, frame, models, {"DT_SG_BLOCK": blk}, monkeypatch)
+        got = _accel(name, frame, models, {"DT_SG_BLOCK": blk, "DT_SG_HULL": hull}, monkeypatch)
         assert got["sg_hash"] == base["sg_hash"], blk
         assert got["sg_list_entries"] == base["sg_list_entries"], blk
-    dflt = _accel(name, frame, models, {}, monkeypatch)
+    dflt = _accel(name, frame, models, {"DT_SG_HULL": hull}, monkeypatch)
     assert dflt["sg_hash"] == base["sg_hash"]
     assert dflt["nodes_hash"] == base["nodes_hash"] and dflt["fnodes_hash"] == base["fnodes_hash"]
+
+
+@pytest.mark.parametrize("name,frame,models", ACCEL_SCENES, ids=[s[0] for s in ACCEL_SCENES])
+def test_shadow_grid_hull_culling_only_drops(name, frame, models, monkeypatch):
+    """Hull culling removes list entries and never adds any: off >= blocks (the default) >=
+    blocks + cells, in entries per list cell, and no cell turns into a tree cell."""
+    off = _accel(name, frame, models, {"DT_SG_HULL": "0"}, monkeypatch)
+    blk = _accel(name, frame, models, {}, monkeypatch)
+    cel = _accel(name, frame, models, {"DT_SG_HULL": "2"}, monkeypatch)
+    assert off["sg_cells"] == blk["sg_cells"] == cel["sg_cells"]
+    assert off["sg_tree_cells"] >= blk["sg_tree_cells"] >= cel["sg_tree_cells"]
+    per = [d["sg_list_entries"] / max(d["sg_cells"] - d["sg_tree_cells"], 1) for d in (off, blk, cel)]
+    if off["sg_tree_cells"] == 0:
+        assert per[0] >= per[1] >= per[2]
 
 
 @pytest.mark.parametrize("name,frame,models", ACCEL_SCENES[:1] + ACCEL_SCENES[2:],

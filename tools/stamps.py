@@ -60,7 +60,17 @@ def main():
             o = 64 + 3 * (li * 256 + sid)
             if arr[o]:
                 rows.append((arr[o], li, sid, arr[o + 1], arr[o + 2]))
+    rows = [r for r in rows if r[2] < 254]
     rows.sort(reverse=True)
+    print("per light: calls/item, active lanes/call, occluded fraction, share of kernel cycles")
+    for li in range(8):
+        o = 64 + 3 * (li * 256 + 255)
+        if arr[o]:
+            sw = sum(r[0] for r in rows if r[1] == li)
+            sl = sum(r[3] for r in rows if r[1] == li)
+            print("  L%d %6.3f %5.1f %6.3f %6.2f%%   shape tests/item %.2f (%.1f lanes each)"
+                  % (li, arr[o] / items, arr[o + 1] / arr[o], arr[o + 2] / max(arr[o + 1], 1),
+                     100.0 * arr[o - 3] / max(tot, 1), sw / items, sl / max(sw, 1)))
     print("top shadow tests (light, shape, type): waves/item lanes/test hit-frac  v0 v2")
     for w, li, sid, ln, hi in rows[:30]:
         sh = d.shapes[sid] if sid < d.n_shapes else None
