@@ -328,7 +328,7 @@ int dt_accel_info_build(const dt_scene_desc* desc, const dt_globals* g, dt_accel
   for (int k = 0; k < 3; ++k) info->sg_dim[k] = a.sg.dim[k];
   info->sg_cells = (int64_t)(a.sg.cells.size() / 2);
   for (size_t c = 0; c + 1 < a.sg.cells.size(); c += 2) {
-    if (a.sg.cells[c + 1] == 0xffffffffu) info->sg_tree_cells++;
+    if (a.sg.cells[c + 1] == DT_SG_WALK) info->sg_tree_cells++;
     else info->sg_list_entries += a.sg.cells[c + 1];
   }
   info->sg_list_pool = (int64_t)a.sg.list.size();
@@ -339,6 +339,7 @@ int dt_accel_info_build(const dt_scene_desc* desc, const dt_globals* g, dt_accel
   info->sg_contents_hash = sg_hash(a.sg, true);
   info->bump_pad = a.bump_pad;
   info->sg_reach = a.sg.reach;
+  info->sg_umbra_cells = a.sg.umbra_cells;
   return DT_OK;
 }
 

@@ -1437,7 +1437,8 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       const int c0 = ((int)z0 * P.sg_dim[1] + (int)y0) * P.sg_dim[0] + (int)x0;
       const DT_CAS uint32_t* e = cas(S.sg_cells) + 2 * (size_t)(P.sg_base[li] + c0);
       const uint32_t off = e[0], n = e[1];
-      if (n != 0xffffffffu) {
+      if (off & DT_SG_UMBRA) return true;   // every segment of the cell crosses one face (host_shadowgrid.cpp)
+      if (n != DT_SG_WALK) {
         DT_CNT(35);
         return bump_list ? occluded_list<true>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, off, n, cnt)
                          : occluded_list<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, off, n, cnt);
@@ -1455,10 +1456,11 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
         const uint2 e = ((const uint2*)S.sg_cells)[(size_t)P.sg_base[li] + cl];
         loff = e.x;
         ln = e.y;
-        lin = ln != 0xffffffffu;
+        lin = ln != DT_SG_WALK;
       }
       DT_CNT(40);
       if (!lin) ln = 0;
+      loff &= ~DT_SG_UMBRA;   // an umbra cell's list holds its occluding face's leaf
       const unsigned long long out_lanes = __ballot(active && !lin);
 #if DT_SG_MIXED
       // lanes with a list take the union; the rest (outside the grid, or in a cell whose list is

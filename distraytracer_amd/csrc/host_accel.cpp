@@ -104,14 +104,14 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
     size_t cells = a.sg.cells.size() / 2, tree = 0, sum = 0, mx = 0;
     for (size_t c = 0; c < cells; ++c) {
       const uint32_t n = a.sg.cells[2 * c + 1];
-      if (n == 0xffffffffu) { ++tree; continue; }
+      if (n == DT_SG_WALK) { ++tree; continue; }
       sum += n;
       mx = std::max(mx, (size_t)n);
     }
     fprintf(stderr, "shadow grid: lights %d dim %dx%dx%d cells %zu (tree %zu) mean list %.2f max %zu list pool %zu "
-            "plane-culled %ld ypad %g hash %016llx\n",
+            "plane-culled %ld umbra cells %ld ypad %g hash %016llx\n",
             a.sg.n_lights, a.sg.dim[0], a.sg.dim[1], a.sg.dim[2], cells, tree,
-            cells > tree ? (double)sum / (cells - tree) : 0.0, mx, a.sg.list.size(), a.sg.plane_dropped, a.sg.ypad,
+            cells > tree ? (double)sum / (cells - tree) : 0.0, mx, a.sg.list.size(), a.sg.plane_dropped, a.sg.umbra_cells, a.sg.ypad,
             (unsigned long long)sg_hash(a.sg, false));
   }
   stage("shadow grid");
@@ -131,8 +131,9 @@ uint64_t sg_hash(const ShadowGrid& sg, bool contents_only)
   }
   std::vector<int32_t> tmp;
   for (size_t c = 0; c + 1 < sg.cells.size(); c += 2) {
-    const uint32_t off = sg.cells[c], n = sg.cells[c + 1];
-    if (n == 0xffffffffu) { mix(0xffffffffu); continue; }
+    const uint32_t off = sg.cells[c] & ~DT_SG_UMBRA, n = sg.cells[c + 1];
+    if (n == DT_SG_WALK) { mix(n); continue; }
+    if (sg.cells[c] & DT_SG_UMBRA) mix(DT_SG_UMBRA);
     tmp.assign(sg.list.begin() + off, sg.list.begin() + off + n);
     std::sort(tmp.begin(), tmp.end());
     mix(n);

@@ -35,10 +35,11 @@ struct ShadowGrid {
   int dim[3] = {0, 0, 0};
   float lo[3] = {0, 0, 0}, inv_h[3] = {0, 0, 0};
   float reach = 0.5f;                // a cell's list covers points this many cells outside it
-  std::vector<uint32_t> cells;       // (offset into list, count | 0xffffffff: walk the tree) per cell
+  std::vector<uint32_t> cells;       // (offset into list | DT_SG_UMBRA, count | DT_SG_WALK) per cell
   std::vector<int32_t> list;         // leaf node indices (reference tree)
   double ypad = 0;                   // lists also hold for blur passes with |shift| <= ypad
   long plane_dropped = 0;            // (leaf, cell) pairs left out by plane culling (diagnostic)
+  long umbra_cells = 0;              // (light, cell) records flagged DT_SG_UMBRA (diagnostic)
 };
 struct FlatScene;
 bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene& fs, ShadowGrid& g,

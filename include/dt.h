@@ -262,6 +262,7 @@ typedef struct dt_accel_info {
   uint64_t sg_hash;            /* cells + list pool in storage order */
   uint64_t sg_contents_hash;   /* each cell's list as a sorted set (order-free) */
   float bump_pad, sg_reach;
+  int64_t sg_umbra_cells;      /* (light, cell) records whose every segment to the light is occluded */
 } dt_accel_info;
 int dt_accel_info_build(const dt_scene_desc* desc, const dt_globals* g, dt_accel_info* info);
 

@@ -247,9 +247,9 @@ def test_shadow_grid_matches_tree_walks(cuda, monkeypatch):
     # themselves) and the likely-occluder list order (any-hit: the image must not change)
     variants = [{"DT_SG_CELLS": "32768", "DT_SG_REACH": "0.5"}, {"DT_SG_CELLS": "4096", "DT_SG_REACH": "2"}]
     variants += [{"DT_SG_BLOCK": b, "DT_SG_ORDER": o} for b in ("0", "4x2", "32x8") for o in ("0", "1")]
-    variants += [{"DT_SG_ORDER": "1"}, {"DT_SG_HULL": "0"}, {"DT_SG_HULL": "2"}]
+    variants += [{"DT_SG_ORDER": "1"}, {"DT_SG_HULL": "0"}, {"DT_SG_HULL": "2"}, {"DT_SG_UMBRA": "0"}, {"DT_SG_UMBRA": "2"}]
     for env in variants:
-        for k in ("DT_SG_CELLS", "DT_SG_REACH", "DT_SG_BLOCK", "DT_SG_ORDER", "DT_SG_HULL"):
+        for k in ("DT_SG_CELLS", "DT_SG_REACH", "DT_SG_BLOCK", "DT_SG_ORDER", "DT_SG_HULL", "DT_SG_UMBRA"):
             monkeypatch.delenv(k, raising=False)
         monkeypatch.setenv("DT_SHADOW_GRID", "1")
         for k, v in env.items():

@@ -156,7 +156,7 @@ def test_oracle_sky_image_cloud_anchor():
 # ---- acceleration structures built on the host (dt_accel_info_build) ------------------------
 
 def _accel(name, frame, models, env, monkeypatch):
-    for k in ("DT_SG_BLOCK", "DT_SG_ORDER", "DT_SG_HULL"):
+    for k in ("DT_SG_BLOCK", "DT_SG_ORDER", "DT_SG_HULL", "DT_SG_UMBRA"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -176,14 +176,16 @@ def test_shadow_grid_block_tests_give_identical_lists(name, frame, models, hull,
     """The per-block (leaf, cell) rejection (host_shadowgrid.cpp) is exact only while the swept
     test, the plane separation and the hull separation stay monotone in the cell box: with hull
     culling off (0) or on every cell (2), every block size must give the per-cell build's lists
-    bit for bit (cells, counts and pool, in storage order)."""
-    base = _accel(name, frame, models, {"DT_SG_BLOCK": "0", "DT_SG_HULL": hull}, monkeypatch)
+    bit for bit (cells, counts and pool, in storage order). Umbra cells off: their default marks
+    whole blocks, by design coarser for larger blocks."""
+    env = {"DT_SG_HULL": hull, "DT_SG_UMBRA": "0"}
+    base = _accel(name, frame, models, dict(env, DT_SG_BLOCK="0"), monkeypatch)
     assert base["sg_lights"] > 0 and base["sg_list_entries"] > 0
     for blk in ("4x2", "8x4", "32x8", "1x1"):
-        got = _accel(name, frame, models, {"DT_SG_BLOCK": blk, "DT_SG_HULL": hull}, monkeypatch)
+        got = _accel(name, frame, models, dict(env, DT_SG_BLOCK=blk), monkeypatch)
         assert got["sg_hash"] == base["sg_hash"], blk
         assert got["sg_list_entries"] == base["sg_list_entries"], blk
-    dflt = _accel(name, frame, models, {"DT_SG_HULL": hull}, monkeypatch)
+    dflt = _accel(name, frame, models, env, monkeypatch)
     assert dflt["sg_hash"] == base["sg_hash"]
     assert dflt["nodes_hash"] == base["nodes_hash"] and dflt["fnodes_hash"] == base["fnodes_hash"]
 
@@ -200,6 +202,21 @@ def test_shadow_grid_hull_culling_only_drops(name, frame, models, monkeypatch):
     per = [d["sg_list_entries"] / max(d["sg_cells"] - d["sg_tree_cells"], 1) for d in (off, blk, cel)]
     if off["sg_tree_cells"] == 0:
         assert per[0] >= per[1] >= per[2]
+
+
+def test_shadow_grid_umbra_cells(monkeypatch):
+    """C3's window point light sits behind the wall the window is cut into: whole blocks of cells
+    see it only through one prism face (host_shadowgrid.cpp umbra cells). Off: none; blocks (the
+    default); blocks + single cells: a superset. Each umbra cell keeps a one-leaf list, so the
+    lists only shrink."""
+    off = _accel("c3", 240, 0, {"DT_SG_UMBRA": "0"}, monkeypatch)
+    blk = _accel("c3", 240, 0, {}, monkeypatch)
+    cel = _accel("c3", 240, 0, {"DT_SG_UMBRA": "2"}, monkeypatch)
+    assert off["sg_umbra_cells"] == 0
+    assert blk["sg_umbra_cells"] >= off["sg_cells"] // off["sg_lights"] // 2
+    assert cel["sg_umbra_cells"] >= blk["sg_umbra_cells"]
+    assert off["sg_list_entries"] > blk["sg_list_entries"] >= cel["sg_list_entries"]
+    assert off["sg_tree_cells"] == blk["sg_tree_cells"] == 0
 
 
 @pytest.mark.parametrize("name,frame,models", ACCEL_SCENES[:1] + ACCEL_SCENES[2:],
