@@ -128,7 +128,9 @@ struct dt_scene {
   bool copy_pending = false;
   bool timed = false;
   // primary-ray candidate lists, rebuilt when the camera / resolution changes (host_primlists.cpp)
-  std::vector<dtd::DNodeDev> fnodes_host;
+  std::vector<dtd::DNodeDev> fnodes_host, bnodes_host;
+  std::vector<std::vector<P3>> fhull, bhull;   // leaf hull points per fast / bump tree node (host_hull.cpp)
+  bool pl_bump = false;                        // lists for the blur passes follow the pass-0 lists
   std::vector<double> pl_key;
   PrimLists pl;
   bool pl_ok = false;
@@ -230,6 +232,16 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
   s->boxes_ordered = acc.boxes_ordered;
   s->sg = std::move(acc.sg);
   s->fnodes_host = acc.fnodes;
+  s->bnodes_host = acc.bnodes;
+  {   // leaf hulls for the primary lists' hull culling (host_primlists.cpp); the bump tree's with
+      // the moving rectangles' shifted corners
+    s->fhull.assign(s->fnodes_host.size(), {});
+    s->bhull.assign(s->bnodes_host.size(), {});
+    for (int i = 0; i < s->n_fnodes; ++i)
+      if (s->fnodes_host[i].meta & dtd::DN_LEAF) leaf_hull_points(f, s->fnodes_host[i], -1, 0.0, s->fhull[i]);
+    for (int i = 0; i < s->n_bnodes; ++i)
+      if (s->bnodes_host[i].meta & dtd::DN_LEAF) leaf_hull_points(f, s->bnodes_host[i], -1, (double)s->bump_pad, s->bhull[i]);
+  }
   if ((rc = upload(s->sg.cells, &s->d_sg_cells)) || (rc = upload(s->sg.list, &s->d_sg_list))) {
     dt_scene_destroy(s);
     return rc;
@@ -395,18 +407,40 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
 // is replaced after the device has drained, since earlier launches may still read it.
 static int update_primary_lists(dt_scene* sc, dtd::DParams& P)
 {
-  P.pl_block = P.pl_nbx = P.pl_nby = 0;
+  P.pl_block = P.pl_nbx = P.pl_nby = P.pl_bump = 0;
   const char* e = getenv("DT_PRIM_LISTS");
   if ((e && e[0] == '0') || sc->n_fnodes <= 0 || !(sc->ftree_mode & 1)) return DT_OK;
   const char* b = getenv("DT_PL_BLOCK");
   const int B = b && atoi(b) > 0 ? atoi(b) : 8;
+  // DT_PL_HULL=0: no hull culling; DT_PL_SUPER: blocks per super-block side (8); DT_PL_BUMP=0: the
+  // blur passes walk the bump tree instead of taking lists
+  const char* ph = getenv("DT_PL_HULL");
+  const bool hull = !(ph && ph[0] == '0');
+  const char* ps = getenv("DT_PL_SUPER");
+  const int SB = ps && atoi(ps) > 0 ? atoi(ps) : 8;
+  const char* pb = getenv("DT_PL_BUMP");
+  const bool bump = !(pb && pb[0] == '0') && sc->n_bnodes > 0;
   std::vector<double> key = {(double)B, (double)P.xRes, (double)P.yRes, (double)P.l, (double)P.r, (double)P.t,
-                             (double)P.b, (double)P.focal_length, (double)P.near_plane, (double)P.aperture};
+                             (double)P.b, (double)P.focal_length, (double)P.near_plane, (double)P.aperture,
+                             (double)hull, (double)SB, (double)bump};
   for (int k = 0; k < 3; ++k) key.insert(key.end(), {P.eye[k], P.X[k], P.Y[k], P.Z[k]});
   if (key != sc->pl_key) {
     HIPCHK(hipDeviceSynchronize());
     sc->pl_key = key;
-    sc->pl_ok = build_primary_lists(sc->fnodes_host, sc->n_fnodes, P, B, sc->pl);
+    sc->pl_ok = build_primary_lists(sc->fnodes_host, sc->n_fnodes, P, B, sc->pl, hull ? &sc->fhull : nullptr, SB);
+    sc->pl_bump = false;
+    PrimLists pb_lists;
+    if (sc->pl_ok && bump &&
+        build_primary_lists(sc->bnodes_host, sc->n_bnodes, P, B, pb_lists, hull ? &sc->bhull : nullptr, SB)) {
+      // the blur passes' lists follow: cells nblk.. 2 nblk - 1, entries after the pass-0 pool
+      const uint32_t base = (uint32_t)(sc->pl.list.size() / 2);
+      for (size_t c = 0; c < pb_lists.cells.size(); c += 2) {
+        sc->pl.cells.push_back(pb_lists.cells[c] + base);
+        sc->pl.cells.push_back(pb_lists.cells[c + 1]);
+      }
+      sc->pl.list.insert(sc->pl.list.end(), pb_lists.list.begin(), pb_lists.list.end());
+      sc->pl_bump = true;
+    }
     if (sc->d_pl_cells) (void)hipFree(sc->d_pl_cells);
     if (sc->d_pl_list) (void)hipFree(sc->d_pl_list);
     sc->d_pl_cells = sc->d_pl_list = nullptr;
@@ -423,6 +457,7 @@ static int update_primary_lists(dt_scene* sc, dtd::DParams& P)
     P.pl_block = sc->pl.block;
     P.pl_nbx = sc->pl.nbx;
     P.pl_nby = sc->pl.nby;
+    P.pl_bump = sc->pl_bump ? 1 : 0;
   }
   return DT_OK;
 }

@@ -1146,9 +1146,11 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
 // order of the smallest ray parameter each leaf's box can be reached at: once every lane's best hit
 // lies before the next entry, no later leaf can change a result. Same box filter, shape tests and
 // tie rule (reference rank) as the fast-tree walk.
-template <class CNT>
+// BUMP: a motion-blur pass over the bump tree's lists: padded leaf boxes, then the exact bumped
+// gather (bump_leaf_gathered) and the shifted shapes, as in the bump-tree walk.
+template <bool BUMP, class CNT>
 __device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams& P, const Walk& w, bool active, V3 ray,
-                                                  V3 org, HitRec& h, uint32_t off, uint32_t n, CNT& cnt)
+                                                  V3 org, float shift, HitRec& h, uint32_t off, uint32_t n, CNT& cnt)
 {
   float t_dist = FLT_MAX;
   bool any = false;
@@ -1162,9 +1164,10 @@ __device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams
     const uint32_t node = __builtin_amdgcn_readfirstlane(cas(S.pl_list)[2 * (size_t)(off + k)]);
     const float tn = __uint_as_float(__builtin_amdgcn_readfirstlane(cas(S.pl_list)[2 * (size_t)(off + k) + 1]));
     if (!__ballot(active && !(h.t_min < tn))) break;
-    const DNodeDev nd = cas(S.fnodes)[node];
+    const DNodeDev nd = cas(BUMP ? S.bnodes : S.fnodes)[node];
     const float tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
     bool hb = active & node_hit<false>(w, nd, 0.0f, org, tcull);
+    if (BUMP && __ballot(hb)) hb = hb & bump_leaf_gathered(S, w, nd.skip, shift, org);
     DT_WORK(cnt.wnodes++; cnt.box += active);
     DT_CNT(26);
     if (__ballot(hb)) {
@@ -1179,7 +1182,7 @@ __device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams
         if (hb) {
           DT_WORK(cnt.prim++);
           int ins = 0, cc = -1;
-          if (shape_hit(S, sid, type, flags, cas(S.geom) + off2, ray, org, 0.0f, t_dist, ins, cc, h.edge)) {
+          if (shape_hit(S, sid, type, flags, cas(S.geom) + off2, ray, org, BUMP ? shift : 0.0f, t_dist, ins, cc, h.edge)) {
             any = true;
             if (t_dist < h.t_min || (t_dist == h.t_min && rank < h.rank)) {
               h.rank = rank;
@@ -1204,9 +1207,12 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
   if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift)))
     return closest_hit_walk<1>(S, P, w, active, ray, org, shift, h, cnt);
   bool any;
-  if (pblock >= 0 && !w.bump_wave) {
-    const uint32_t off = cas(S.pl_cells)[2 * pblock], n = cas(S.pl_cells)[2 * pblock + 1];
-    any = closest_hit_plist(S, P, w, active, ray, org, h, off, n, cnt);
+  if (pblock >= 0 && (!w.bump_wave || P.pl_bump)) {
+    // blur passes take the bump tree's lists, stored after the pass-0 lists
+    const int cell = w.bump_wave ? pblock + P.pl_nbx * P.pl_nby : pblock;
+    const uint32_t off = cas(S.pl_cells)[2 * cell], n = cas(S.pl_cells)[2 * cell + 1];
+    any = w.bump_wave ? closest_hit_plist<true>(S, P, w, active, ray, org, shift, h, off, n, cnt)
+                      : closest_hit_plist<false>(S, P, w, active, ray, org, 0.0f, h, off, n, cnt);
   } else {
     any = w.bump_wave ? closest_hit_walk<2>(S, P, w, active, ray, org, shift, h, cnt)
                       : closest_hit_walk<0>(S, P, w, active, ray, org, shift, h, cnt);
@@ -1693,10 +1699,11 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
 #ifdef DT_STAMPS
     const unsigned long long v_before = cnt.ph[26];
 #endif
-    // primary rays of a pass without a shift: the pixel block's candidate list, when the wave's
-    // pixels share one block (host_primlists.cpp)
+    // primary rays: the pixel block's candidate list, when the wave's pixels share one block
+    // (host_primlists.cpp; blur passes take the bump tree's lists when they were built)
     int pblock = -1;
-    if (P.pl_block > 0 && __ballot(is_root) && !__ballot(have && shift != 0.0f) && P.n_fnodes > 0 && (P.ftree_mode & 1)) {
+    if (P.pl_block > 0 && __ballot(is_root) && (P.pl_bump || !__ballot(have && shift != 0.0f)) && P.n_fnodes > 0 &&
+        (P.ftree_mode & 1)) {
       const int px = (int)(c.rng.pixel % (uint32_t)P.xRes), py = (int)(c.rng.pixel / (uint32_t)P.xRes);
       const int blk = (py / P.pl_block) * P.pl_nbx + px / P.pl_block;
       const int b0 = uni(blk);

@@ -125,6 +125,7 @@ struct DParams {
   int32_t ftree_mode;     // walks that use it: bit 0 closest hit, bit 1 shadow
   int32_t boxes_ordered;  // every node of both trees has lb <= ub (finite walks take slab ends by min/max)
   int32_t pl_block, pl_nbx, pl_nby;   // primary-ray candidate lists per pl_block^2 pixels (0: none)
+  int32_t pl_bump;                     // 1: blur-pass lists (bump tree) follow, cells pl_nbx*pl_nby on
   int32_t n_cloud_steps;
   int32_t item_batch;     // wave items per queue atomic (dt_api.cpp: 2 when waves take >= 64 items, else 1)
   uint32_t seed;

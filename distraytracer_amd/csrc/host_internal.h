@@ -3,6 +3,7 @@
 #include <cstdint>
 #include <functional>
 #include <string>
+#include <array>
 #include <vector>
 
 #include "../../include/dt.h"
@@ -42,6 +43,23 @@ struct ShadowGrid {
   long umbra_cells = 0;              // (light, cell) records flagged DT_SG_UMBRA (diagnostic)
 };
 struct FlatScene;
+
+// host_hull.cpp: convex-hull separation (exact culling of shadow-grid and primary-ray lists)
+using P3 = std::array<double, 3>;
+inline double dot3(const P3& a, const P3& b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+inline P3 sub3(const P3& a, const P3& b) { return {a[0] - b[0], a[1] - b[1], a[2] - b[2]}; }
+inline P3 mad3(const P3& a, const P3& b, double s) { return {a[0] + s * b[0], a[1] + s * b[1], a[2] + s * b[2]}; }
+// points whose hull holds every hit a planar shape's float tests can report (moving named
+// rectangles: also shifted by +-ypad in y); false for spheres and cylinders
+bool shape_hull_points(const dtd::DShapeHdr& h, const double* g, double ypad, std::vector<P3>& pts);
+// the hull points of a leaf's shapes but `skip_shape`; false (empty) when one has none
+bool leaf_hull_points(const FlatScene& fs, const dtd::DNodeDev& leaf, int skip_shape, double ypad, std::vector<P3>& out);
+// min over A minus max over B of the projections on v, in units of |v|
+double hull_gap(const P3* A, int na, const P3* B, int nb, const P3& v);
+// are the hulls of A and B more than `margin` apart? (GJK direction, then the exact gap along it;
+// `hint`: a direction tried first, returned as the one GJK ended with)
+bool hulls_separated(const P3* A, int na, const P3* B, int nb, double margin, P3& hint);
+
 bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene& fs, ShadowGrid& g,
                        double target_cells = 32768, float reach = 0.5f, double ypad = 0);
 
@@ -85,8 +103,10 @@ struct PrimLists {
   std::vector<uint32_t> cells;   // (first entry, count) per block
   std::vector<uint32_t> list;    // (fast-tree node, float bits of t_near) per entry
 };
+// hulls: per tree node, the leaf's shape hull points (host_hull.cpp; empty: never culled), or null;
+// SB: blocks per super-block side
 bool build_primary_lists(const std::vector<dtd::DNodeDev>& fnodes, int n_fnodes, const dtd::DParams& P, int B,
-                         PrimLists& out);
+                         PrimLists& out, const std::vector<std::vector<P3>>* hulls = nullptr, int SB = 8);
 
 // camera / params (host_flatten.cpp)
 int fill_params(const dt_globals& g, int frame, const dt_tiles* tiles, dtd::DParams& P, std::string& err);

@@ -15,6 +15,19 @@
 // always contains the leaf of the closest hit; closest-hit ties go to the lower reference rank, as
 // on the fast tree. The margins below (1e-6 relative) lie far above the rounding of the double camera
 // arithmetic; the float pixel coordinates are recomputed exactly as the device computes them.
+//
+// Super-blocks and hull culling: the tree is walked once per super-block (SB x SB blocks) and each
+// block filters the super-block's leaves with its own frustum, which yields the same lists as a walk
+// per block (the block's frustum lies inside the super-block's, and the walk order is kept). With
+// `hulls`, a super-block also drops the leaves whose shapes' hull (host_hull.cpp) stays more than a
+// margin away from the hull of its rays: the eye-sample square's corners and the points the rays
+// reach at the depth of the scene's far end (every ray point up to there is a convex combination of
+// the two). No primary ray of the super-block can then report a hit on those shapes, so the closest
+// hit never comes from them. The margin (1e-3 plus 1e-5 of the scene scale) covers the f32 ray
+// parameters of the shape tests (~1e-7 of the distance) and the camera rounding.
+//
+// Motion-blur passes use lists built over the bump tree (padded leaf boxes; leaf hulls with the
+// moving rectangles' shifted corners), tested with the exact bumped gather on the device.
 #include <algorithm>
 #include <array>
 #include <cmath>
@@ -78,11 +91,12 @@ bool frustum_meets(const Frustum& F, const double b[6], double& tnear)
 }  // namespace
 
 bool build_primary_lists(const std::vector<dtd::DNodeDev>& fnodes, int n_fnodes, const dtd::DParams& P, int B,
-                         PrimLists& out)
+                         PrimLists& out, const std::vector<std::vector<P3>>* hulls, int SB)
 {
   out = PrimLists();
   if (n_fnodes <= 0 || B < 1 || P.xRes < 1 || P.yRes < 1) return false;
   if (!(P.focal_length > 0) || !(P.near_plane > 0) || !(P.aperture >= 0)) return false;
+  if (SB < 1) SB = 1;
   const double X[3] = {P.X[0], P.X[1], P.X[2]}, Y[3] = {P.Y[0], P.Y[1], P.Y[2]}, Z[3] = {P.Z[0], P.Z[1], P.Z[2]};
   const double* eye = P.eye;
   double scale = 1;
@@ -93,6 +107,7 @@ bool build_primary_lists(const std::vector<dtd::DNodeDev>& fnodes, int n_fnodes,
   const double m = 1e-6 * (1 + scale);
   // camera-space boxes of every node (the AABB of its 8 corners), widened by m
   std::vector<std::array<double, 6>> cb(n_fnodes);
+  double wmax = 0;   // camera depth of the scene's far end (root box)
   for (int i = 0; i < n_fnodes; ++i) {
     const dtd::DNodeDev& nd = fnodes[i];
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -111,6 +126,7 @@ bool build_primary_lists(const std::vector<dtd::DNodeDev>& fnodes, int n_fnodes,
       cb[i][2 * k] = lo[k] - m;
       cb[i][2 * k + 1] = hi[k] + m;
     }
+    if (i == 0) wmax = hi[2];
   }
   out.block = B;
   out.nbx = (P.xRes + B - 1) / B;
@@ -121,39 +137,86 @@ bool build_primary_lists(const std::vector<dtd::DNodeDev>& fnodes, int n_fnodes,
   // the device's float pixel coordinates (camera_ray): a = l + (r - l) * x / xRes
   auto acoord = [&](int x) { return P.l + (P.r - P.l) * (float)x / (float)P.xRes; };
   auto bcoord = [&](int y) { return P.b + (P.t - P.b) * (float)y / (float)P.yRes; };
-  const int nthr = std::max(1, std::min({(int)std::thread::hardware_concurrency(), out.nby, 16}));
+  const double rho = (double)P.aperture * 0.5 * (1 + 1e-6) + 1e-7;
+  // the frustum of the pixels [x0, x1] x [y0, y1] (and their a, b ranges)
+  auto frustum = [&](int x0, int x1, int y0, int y1, double ab[4]) {
+    const double a0 = std::min(acoord(x0), acoord(x1)), a1 = std::max(acoord(x0), acoord(x1));
+    const double b0 = std::min(bcoord(y0), bcoord(y1)), b1 = std::max(bcoord(y0), bcoord(y1));
+    ab[0] = a0; ab[1] = a1; ab[2] = b0; ab[3] = b1;
+    Frustum F;
+    const double ma = 1e-6 * (1 + std::fabs(f) * std::max(std::fabs(a0), std::fabs(a1))) + m;
+    const double mb = 1e-6 * (1 + std::fabs(f) * std::max(std::fabs(b0), std::fabs(b1))) + m;
+    F.fa0 = f * a0 - ma;
+    F.fa1 = f * a1 + ma;
+    F.fb0 = f * b0 - mb;
+    F.fb1 = f * b1 + mb;
+    F.rho = rho;
+    F.fn = f * (double)P.near_plane * (1 - 1e-9);
+    return F;
+  };
+  // hull culling (header): the rays' points up to parameter T, where they pass the far end
+  const double T = std::max(1.0, (wmax + 1.0) / (f * (double)P.near_plane));
+  const double mhull = 1e-3 + 1e-5 * (1 + scale);
+  const int nsbx = (out.nbx + SB - 1) / SB, nsby = (out.nby + SB - 1) / SB;
+  const int nthr = std::max(1, std::min({(int)std::thread::hardware_concurrency(), nsby, 16}));
   auto work = [&](int t) {
-    for (int by = out.nby * t / nthr; by < out.nby * (t + 1) / nthr; ++by)
-      for (int bx = 0; bx < out.nbx; ++bx) {
-        const int x0 = bx * B, x1 = std::min(P.xRes, x0 + B) - 1;
-        const int y0 = by * B, y1 = std::min(P.yRes, y0 + B) - 1;
-        const double a0 = std::min(acoord(x0), acoord(x1)), a1 = std::max(acoord(x0), acoord(x1));
-        const double b0 = std::min(bcoord(y0), bcoord(y1)), b1 = std::max(bcoord(y0), bcoord(y1));
-        Frustum F;
-        const double ma = 1e-6 * (1 + std::fabs(f) * std::max(std::fabs(a0), std::fabs(a1))) + m;
-        const double mb = 1e-6 * (1 + std::fabs(f) * std::max(std::fabs(b0), std::fabs(b1))) + m;
-        F.fa0 = f * a0 - ma;
-        F.fa1 = f * a1 + ma;
-        F.fb0 = f * b0 - mb;
-        F.fb1 = f * b1 + mb;
-        F.rho = (double)P.aperture * 0.5 * (1 + 1e-6) + 1e-7;
-        F.fn = f * (double)P.near_plane * (1 - 1e-9);
-        std::vector<std::pair<float, int32_t>>& L = lists[(size_t)by * out.nbx + bx];
+    std::vector<int32_t> cand;
+    std::vector<P3> A(20);
+    P3 hint = {0, 0, 0};
+    for (int sby = nsby * t / nthr; sby < nsby * (t + 1) / nthr; ++sby)
+      for (int sbx = 0; sbx < nsbx; ++sbx) {
+        const int bx0 = sbx * SB, bx1 = std::min(out.nbx, bx0 + SB) - 1;
+        const int by0 = sby * SB, by1 = std::min(out.nby, by0 + SB) - 1;
+        double ab[4];
+        const Frustum FS = frustum(bx0 * B, std::min(P.xRes, (bx1 + 1) * B) - 1, by0 * B,
+                                   std::min(P.yRes, (by1 + 1) * B) - 1, ab);
+        cand.clear();
         int i = 0;
         while (i < n_fnodes) {
           double tn;
-          const bool hit = frustum_meets(F, cb[i].data(), tn);
+          const bool hit = frustum_meets(FS, cb[i].data(), tn);
           if (fnodes[i].meta & dtd::DN_LEAF) {
-            // conservative float t: rounded down, less a relative margin
-            if (hit) L.push_back({(float)(tn * (1 - 1e-6)) - 1e-6f, (int32_t)i});
+            if (hit) cand.push_back(i);
             ++i;
           } else {
             i = hit ? i + 1 : fnodes[i].skip;
           }
         }
-        std::stable_sort(L.begin(), L.end(), [](const std::pair<float, int32_t>& p, const std::pair<float, int32_t>& q) {
-          return p.first < q.first;
-        });
+        if (hulls) {
+          for (int k = 0; k < 4; ++k) {   // eye-sample corners, then the far points
+            const double ex = (k & 1) ? rho : -rho, ey = (k & 2) ? rho : -rho;
+            for (int a = 0; a < 3; ++a) A[k][a] = eye[a] + ex * X[a] + ey * Y[a];
+          }
+          for (int k = 0; k < 4; ++k)
+            for (int j = 0; j < 4; ++j) {
+              const double a = ab[j & 1], b = ab[2 + (j >> 1)];
+              P3& q = A[4 + 4 * k + j];
+              for (int c = 0; c < 3; ++c) {
+                const double F = eye[c] + f * (a * X[c] + b * Y[c] - (double)P.near_plane * Z[c]);
+                q[c] = A[k][c] + T * (F - A[k][c]);
+              }
+            }
+          size_t w = 0;
+          for (int32_t leaf : cand) {
+            const std::vector<P3>& hl = (*hulls)[leaf];
+            if (!hl.empty() && hulls_separated(A.data(), 20, hl.data(), (int)hl.size(), mhull, hint)) continue;
+            cand[w++] = leaf;
+          }
+          cand.resize(w);
+        }
+        for (int by = by0; by <= by1; ++by)
+          for (int bx = bx0; bx <= bx1; ++bx) {
+            const Frustum F = frustum(bx * B, std::min(P.xRes, bx * B + B) - 1, by * B, std::min(P.yRes, by * B + B) - 1, ab);
+            std::vector<std::pair<float, int32_t>>& L = lists[(size_t)by * out.nbx + bx];
+            for (int32_t leaf : cand) {
+              double tn;
+              // conservative float t: rounded down, less a relative margin
+              if (frustum_meets(F, cb[leaf].data(), tn)) L.push_back({(float)(tn * (1 - 1e-6)) - 1e-6f, leaf});
+            }
+            std::stable_sort(L.begin(), L.end(), [](const std::pair<float, int32_t>& p, const std::pair<float, int32_t>& q) {
+              return p.first < q.first;
+            });
+          }
       }
   };
   std::vector<std::thread> pool;

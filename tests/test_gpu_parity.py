@@ -286,6 +286,7 @@ PL_CASES = [  # (name, builder, frame, models, W, H, spp, depth, window)
     ("c4-models", "final", 240, 1, 1920, 1080, 16, 3, (1200, 500, 1296, 580)),
     ("c1-dof", "spheres", 0, 0, 256, 256, 16, 2, (64, 64, 192, 192)),
     ("c5-tunnel", "final", 1200, 0, 320, 180, 16, 3, (96, 40, 224, 136)),
+    ("c5-tunnel-1680", "final", 1680, 0, 320, 180, 16, 3, (96, 40, 224, 136)),
     ("c2-full", "final", 240, 0, 200, 150, 4, 4, (0, 0, 200, 150)),
 ]
 
@@ -294,7 +295,9 @@ PL_CASES = [  # (name, builder, frame, models, W, H, spp, depth, window)
 def test_primary_lists_match_tree_walks(cuda, monkeypatch, case):
     """Primary rays over their pixel block's candidate leaves (host_primlists.cpp: camera-space
     frustum of the block's DoF rays, leaves sorted by reach, early exit) must give the image of
-    fast-tree walks bit for bit, for any block size (a ragged last block included)."""
+    fast-tree walks bit for bit, for any block size (a ragged last block included), super-block
+    size, with and without hull culling, and with the blur passes (C5 tunnel frames) on the bump
+    tree's lists or on bump-tree walks."""
     name, builder, frame, models, W, H, spp, depth, win = case
     g = dt.globals_default()
     g.use_model = models
@@ -304,11 +307,16 @@ def test_primary_lists_match_tree_walks(cuda, monkeypatch, case):
     monkeypatch.setenv("DT_PRIM_LISTS", "0")
     ref_img, ref_st = _render_gpu(built, g, frame, tile)
     monkeypatch.delenv("DT_PRIM_LISTS")
-    for blk in ("8", "3", "16"):
-        monkeypatch.setenv("DT_PL_BLOCK", blk)
+    variants = [{"DT_PL_BLOCK": b} for b in ("8", "3", "16")]
+    variants += [{"DT_PL_HULL": "0"}, {"DT_PL_SUPER": "1"}, {"DT_PL_SUPER": "3", "DT_PL_BLOCK": "5"}, {"DT_PL_BUMP": "0"}]
+    for env in variants:
+        for k in ("DT_PL_BLOCK", "DT_PL_HULL", "DT_PL_SUPER", "DT_PL_BUMP"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         img, st = _render_gpu(built, g, frame, tile)
-        assert st.rays == ref_st.rays and st.shadow_rays == ref_st.shadow_rays, blk
-        assert np.array_equal(img, ref_img), blk
+        assert st.rays == ref_st.rays and st.shadow_rays == ref_st.shadow_rays, env
+        assert np.array_equal(img, ref_img), env
 
 
 @pytest.mark.parametrize("n", [150, 210])
