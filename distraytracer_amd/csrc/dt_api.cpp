@@ -325,12 +325,23 @@ int dt_accel_info_build(const dt_scene_desc* desc, const dt_globals* g, dt_accel
 {
   if (!desc || !g || !info) return fail(DT_E_INVALID, "null argument");
   if (desc->n_shapes < 0 || (desc->n_shapes > 0 && !desc->shapes)) return fail(DT_E_INVALID, "invalid descriptor");
+  // DT_TIMING=1: host stage times on stderr, as dt_scene_create
+  const bool timing = getenv("DT_TIMING") != nullptr;
+  auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double t_stage = now();
+  auto stage = [&](const char* name) {
+    if (!timing) return;
+    const double t = now();
+    fprintf(stderr, "dt_accel_info_build %-12s %8.2f ms\n", name, t - t_stage);
+    t_stage = t;
+  };
   FlatScene f;
   std::string err;
   int rc = flatten_scene(*desc, *g, f, err);
   if (rc) return fail(rc, err);
+  stage("flatten+bvh");
   Accel a;
-  build_accel(f, *g, a);
+  build_accel(f, *g, a, stage);
   memset(info, 0, sizeof(*info));
   info->n_nodes = (int32_t)a.dnodes.size();
   info->n_fnodes = a.n_fnodes;
