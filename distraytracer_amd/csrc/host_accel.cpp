@@ -53,12 +53,14 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
       o.aux = h.off;
     }
   }
-  // Alternative traversal tree (host_fasttree.cpp): exact by construction. Closest-hit walks use
-  // it by default; for shadow walks the reference's own SAH tree is faster on C3.
-  // DT_FAST_TREE: c (default) closest-hit walks, 1 every fast walk, s shadow walks only, 0 none.
-  // On C3 closest hit walks it faster (1666 vs 1624 Mpixel-samples/s), shadow walks slower.
+  // Alternative traversal tree (host_fasttree.cpp): exact by construction. Every fast walk uses it
+  // by default. DT_FAST_TREE: 1 (default) every fast walk, c closest-hit walks only, s shadow walks
+  // only, 0 none. Round 1 kept shadow walks on the reference tree (C3 1666 vs 1624 then); since the
+  // shadow grid answers nearly every C3 shadow ray, the tree walks left are C4's mesh cells, where
+  // the fast tree is 14% faster end to end (1325 vs 1164 Mpixel-samples/s; C3, C2 and the tunnel
+  // frames within 0.3%, profiles/r02aa_ab_fasttree.log).
   const char* ft = getenv("DT_FAST_TREE");
-  a.ftree_mode = !ft ? 1 : ft[0] == '1' ? 3 : ft[0] == 'c' ? 1 : ft[0] == 's' ? 2 : 0;
+  a.ftree_mode = !ft ? 3 : ft[0] == '1' ? 3 : ft[0] == 'c' ? 1 : ft[0] == 's' ? 2 : 0;
   // DT_EYE_ORDER=0: children in SAH order instead of nearer-to-the-camera first
   const char* eo = getenv("DT_EYE_ORDER");
   const double* eye = (eo && eo[0] == '0') ? nullptr : g.eye;

@@ -217,7 +217,7 @@ def test_slab_layout_matches_image(cuda):
 def test_fast_tree_gathers_the_reference_leaves(cuda, monkeypatch):
     """The alternative traversal tree (host_fasttree.cpp, same leaves under SAH inner nodes) must
     give the reference-tree image bit for bit (monotone slab test + rank tie-break), whichever
-    walks use it: DT_FAST_TREE=0 (none), c (closest hit, the default), s (shadow), 1 (both).
+    walks use it: DT_FAST_TREE=0 (none), c (closest hit), s (shadow), 1 (both, the default).
     C2 window with glossy floor, doors and area-light shadows."""
     g = dt.globals_default()
     g.use_model = 0
