@@ -378,7 +378,7 @@ int64_t dt_slab_floats_max(const dt_globals* g, const dt_tiles* tiles)
 {
   if (!g || !tiles) return -1;
   dt_tiles t = *tiles;
-  t.rank = 0;   // rank 0 owns the most tiles
+  t.rank = 0;   // every rank has the same number of slots (dtd::tile_of)
   return dt_slab_floats(g, &t);
 }
 
@@ -516,6 +516,10 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   // (C2: ~30) the coarser tail costs more (-11%)
   dtd::DParams PL = P;
   PL.item_batch = PL.n_items >= 64 * grid ? 2 : 1;
+  // deep-cascade waves raise their priority (dt_kernels.hip, DT_PRIO_STEPS) when the frame is split
+  // over ranks, where one such wave bounds a rank's kernel; DT_PRIO_STEPS=<n> overrides (0: off)
+  static const char* ps = getenv("DT_PRIO_STEPS");
+  PL.prio_steps = ps ? atoi(ps) : (PL.world > 1 ? 8 : 0);
   memset(sc->h_launch, 0, dt_launch_size());
   memcpy(sc->h_launch + dt_scene_struct_offset(), &hs, sizeof(hs));
   memcpy(sc->h_launch + dt_params_struct_offset(), &PL, sizeof(PL));
@@ -548,7 +552,8 @@ int dt_collect_stats(const dt_scene* sc_c, void* stream, dt_stats* stats)
     // pixels rendered = owned pixels inside the window
     int64_t tiles_y = (P.y1 - P.y0 + P.th - 1) / P.th;
     for (int64_t k = 0; k < P.n_owned_tiles; ++k) {
-      int64_t t = P.rank + k * P.world;
+      int64_t t = dtd::tile_of(k, P.rank, P.world);
+      if (t >= P.n_tiles) continue;
       int ty = (int)(t / P.tiles_x), tx = (int)(t % P.tiles_x);
       (void)tiles_y;
       int w = P.x1 - (P.x0 + tx * P.tw);
@@ -693,9 +698,10 @@ int dt_unpack_slabs(const dt_globals* g, const dt_tiles* tiles, int32_t world, c
     // host scatter
     int64_t ntiles = (int64_t)P.tiles_x * ((P.y1 - P.y0 + P.th - 1) / P.th);
     for (int r = 0; r < world; ++r) {
-      int64_t owned = ntiles > r ? (ntiles - r + world - 1) / world : 0;
+      int64_t owned = (ntiles + world - 1) / world;
       for (int64_t slot = 0; slot < owned; ++slot) {
-        int64_t tid = r + slot * world;
+        int64_t tid = dtd::tile_of(slot, r, world);
+        if (tid >= ntiles) continue;
         int ty = (int)(tid / P.tiles_x), tx = (int)(tid % P.tiles_x);
         for (int py = 0; py < P.th; ++py)
           for (int px = 0; px < P.tw; ++px) {

@@ -70,6 +70,12 @@ using namespace dtd;
 #ifndef DT_SG_COHERENT
 #define DT_SG_COHERENT 1   // waves within reach of one cell test that cell's list (else: union path)
 #endif
+#ifndef DT_PRIO_STEPS
+#define DT_PRIO_STEPS 1    // 1: waves raise their issue priority after P.prio_steps DFS steps (dt_api.cpp)
+#endif
+#ifndef DT_PRIO_LEVEL
+#define DT_PRIO_LEVEL 3
+#endif
 #ifndef DT_SG_MIXED
 #define DT_SG_MIXED 0      // waves with lanes outside the lists: union for the others, then tree walk
 #endif
@@ -1646,6 +1652,9 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
   const DScene& S = *c.S;
   const DParams& P = *c.P;
   int sp = 0;
+#if DT_PRIO_STEPS > 0
+  int prio_steps = 0;
+#endif
   if (active && P.max_depth > 0) {
     Entry e;
     e.a = ray0; e.b = org0; e.k = 1.0f; e.depth = P.max_depth; e.key = rootkey; e._pad = 1;  // root
@@ -1686,6 +1695,15 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     }
     if (!__ballot(have)) break;
     DT_CNT(7);
+#if DT_PRIO_STEPS > 0
+    // A deep glossy cascade (fan-out 2 per bounce, ~100 DFS steps for one lane against ~1.5 on
+    // average; C3 has a column of such pixels) keeps its wave busy up to ~80x the mean item (7.6 ms
+    // of wave time, tools/item_times.py): with the frame split over ranks that one wave bounds a
+    // rank's kernel. Such a wave raises its issue priority once its tree grows long (reset at the
+    // end of the item). C3 at 8 ranks: slowest rank 7.45 -> 6.95 ms; at 1 rank it costs 0.5%, so
+    // the host enables it for tile splits only (P.prio_steps).
+    if (++prio_steps == P.prio_steps) __builtin_amdgcn_s_setprio(DT_PRIO_LEVEL);
+#endif
     const V3 ray = e.a, eye = e.b;
     const int depth = e.depth;
     const float k = e.k;
@@ -2057,11 +2075,11 @@ __device__ __forceinline__ void pixel_of(const DParams& P, int64_t q, int& x, in
   int64_t slot = q / tile_px;
   int local = (int)(q - slot * tile_px);
   int py = local / P.tw, px = local - py * P.tw;
-  int64_t t = (int64_t)P.rank + slot * P.world;
+  int64_t t = tile_of(slot, P.rank, P.world);
   int ty = (int)(t / P.tiles_x), tx = (int)(t - (int64_t)ty * P.tiles_x);
   x = P.x0 + tx * P.tw + px;
   y = P.y0 + ty * P.th + py;
-  valid = slot < P.n_owned_tiles && x < P.x1 && y < P.y1;
+  valid = slot < P.n_owned_tiles && t < P.n_tiles && x < P.x1 && y < P.y1;
   slab_off = q * 3;
 }
 
@@ -2159,6 +2177,9 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     int64_t px_off = 0;
     bool px_valid = false;
     pixel_of(P, item * group + (j < group ? j : 0), px_x, px_y, px_off, px_valid);
+#ifdef DT_ITEM_TIMES
+    const unsigned long long item_t0 = __builtin_amdgcn_s_memtime();
+#endif
 
     for (int chunk = 0; chunk < P.chunks; ++chunk) {
       const int sample = chunk * DT_WAVE + (lane - j * per);
@@ -2265,10 +2286,22 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       pixel_of(P, item * group + lane, qx, qy, qo, qv);
       if (qv) {
         V3 color = divs(v3(psum[0][lane], psum[1][lane], psum[2][lane]), spp);
+#ifdef DT_ITEM_TIMES   // diagnostic builds: the item's wave cycles / 1e4 in every channel
+        color = v3(1, 1, 1);
+        {
+          const float cyc = (float)(__builtin_amdgcn_s_memtime() - item_t0) * 1e-4f;
+          const int64_t off = P.layout == DT_OUT_SLAB ? qo : 3 * ((int64_t)(P.yRes - 1 - qy) * P.xRes + qx);
+          out[off] = cyc; out[off + 1] = cyc; out[off + 2] = cyc;
+        }
+        if (false)
+#endif
         store_pixel(P, out, qx, qy, qo, color);
         if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
       }
     }
+#if DT_PRIO_STEPS > 0
+    if (P.prio_steps > 0) __builtin_amdgcn_s_setprio(0);
+#endif
     ++item;
   }
   {
@@ -2328,15 +2361,15 @@ extern "C" __global__ void dt_unpack_kernel(const DLaunch* __restrict__ Lp, int 
   int r = (int)(q / per_rank);
   int64_t local = q - (int64_t)r * per_rank;
   int64_t ntiles = (int64_t)P.tiles_x * ((P.y1 - P.y0 + P.th - 1) / P.th);
-  int64_t owned = ntiles > r ? (ntiles - r + world - 1) / world : 0;
+  int64_t owned = (ntiles + world - 1) / world;
   const int64_t tile_px = (int64_t)P.tw * P.th;
   int64_t slot = local / tile_px;
   int lp = (int)(local - slot * tile_px);
   int py = lp / P.tw, px = lp - py * P.tw;
-  int64_t t = (int64_t)r + slot * world;
+  int64_t t = tile_of(slot, r, world);
   int ty = (int)(t / P.tiles_x), tx = (int)(t - (int64_t)ty * P.tiles_x);
   int x = P.x0 + tx * P.tw + px, y = P.y0 + ty * P.th + py;
-  bool valid = slot < owned && x < P.x1 && y < P.y1;
+  bool valid = slot < owned && t < ntiles && x < P.x1 && y < P.y1;
   if (!valid) return;
   int64_t off = 3 * ((int64_t)(P.yRes - 1 - y) * P.xRes + x);
   const float* s = slabs + (int64_t)r * slab_floats + local * 3;

@@ -128,6 +128,7 @@ struct DParams {
   int32_t pl_bump;                     // 1: blur-pass lists (bump tree) follow, cells pl_nbx*pl_nby on
   int32_t n_cloud_steps;
   int32_t item_batch;     // wave items per queue atomic (dt_api.cpp: 2 when waves take >= 64 items, else 1)
+  int32_t prio_steps;     // DFS steps after which a wave raises its issue priority (0: never)
   uint32_t seed;
   float aperture, focal_length, near_plane;
   float l, r, t, b;
@@ -137,7 +138,8 @@ struct DParams {
   float frame_f;          // float(frame) as passed to cloudColor
   // tiles
   int32_t x0, y0, x1, y1, tw, th, rank, world, layout, tiles_x;
-  int64_t n_owned_tiles;
+  int64_t n_owned_tiles;  // slots per rank: ceil(n_tiles / world), the last one may hold no tile
+  int64_t n_tiles;
   int64_t n_items;
   // camera
   double eye[3], X[3], Y[3], Z[3];
@@ -146,5 +148,32 @@ struct DParams {
   double sun[3];          // sundir.normalized() (cpp:152)
   double sun_outer[3], sun_inner[3], sun_core[3], bluesky[3], redsky[3];
 };
+
+#ifndef DT_HD
+#if defined(__HIPCC__)
+#define DT_HD __host__ __device__ __forceinline__
+#else
+#define DT_HD inline
+#endif
+#endif
+
+// Tile ownership of the multi-GPU split: the tiles (raster order over the window) fall into groups
+// of `world` consecutive tiles, and slot s of rank r is tile s*world + (r + rot(s)) % world. Every
+// rank takes one tile of every group, like a plain t % world interleave, but each group's ranks
+// are rotated by a hash of the group: with a fixed rotation the interleave aliases with the image
+// rows (1920 px = 60 tiles = 7.5 groups of 8, so ranks r and r+4 took the same tile columns, and
+// at 8 GPUs the two ranks owning the window's columns ran 21% longer than the others).
+DT_HD uint32_t tile_rot(int64_t slot, int world)
+{
+  uint32_t h = (uint32_t)slot * 2654435761u;
+  h ^= h >> 15;
+  h *= 0x2c1b3c6du;
+  h ^= h >> 12;
+  return h % (uint32_t)world;
+}
+DT_HD int64_t tile_of(int64_t slot, int rank, int world)
+{
+  return slot * world + (int64_t)(((uint32_t)rank + tile_rot(slot, world)) % (uint32_t)world);
+}
 
 }  // namespace dtd

@@ -319,7 +319,8 @@ int fill_tiles(const dt_globals& g, const dt_tiles* T, DParams& P, std::string& 
   P.tiles_x = (P.x1 - P.x0 + P.tw - 1) / P.tw;
   int64_t tiles_y = (P.y1 - P.y0 + P.th - 1) / P.th;
   int64_t n_tiles = (int64_t)P.tiles_x * tiles_y;
-  P.n_owned_tiles = P.rank < n_tiles ? (n_tiles - P.rank + P.world - 1) / P.world : 0;
+  P.n_tiles = n_tiles;
+  P.n_owned_tiles = (n_tiles + P.world - 1) / P.world;   // slots (dtd::tile_of): equal for every rank
   return DT_OK;
 }
 

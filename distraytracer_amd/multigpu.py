@@ -1,7 +1,9 @@
 """Image-space tile split across ranks + gather of finished tiles.
 
-Every rank holds the whole (tiny) scene and renders the 32x32 tiles t with t % world == rank
-(interleaved, so the expensive sky/glossy regions spread over all GPUs) into a packed slab.
+Every rank holds the whole (tiny) scene and renders one 32x32 tile of every group of `world`
+consecutive tiles (raster order), the ranks rotated by a hash of the group (dt_scene_dev.h
+tile_of), into a packed slab: the expensive sky/glossy regions spread over all GPUs, and unlike a
+plain t % world interleave no rank is tied to a fixed set of tile columns.
 The only exchange step is one gather of the finished slabs to rank 0 (torch.distributed:
 RCCL over xGMI on the GPU box, gloo in the CPU tests), after which rank 0 scatters the slabs
 into the ppmOut image (dt_unpack_slabs). Sample RNG is keyed on the global pixel index, so the

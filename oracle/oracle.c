@@ -1552,9 +1552,14 @@ static long long out_offset(const dt_globals* g, const dt_tiles* T, int x, int y
   int tiles_x = (x1 - x0 + tw - 1) / tw;
   int tx = (x - x0) / tw, ty = (y - y0) / th;
   long long tid = (long long)ty * tiles_x + tx;
-  if (tid % world != T->rank) return -1;
+  /* multi-GPU tile ownership (dt_scene_dev.h tile_of): group tid / world, ranks rotated by a hash */
+  long long slot = tid / world;
+  unsigned h = (unsigned)slot * 2654435761u;
+  h ^= h >> 15;
+  h *= 0x2c1b3c6du;
+  h ^= h >> 12;
+  if ((long long)(((unsigned)(tid % world) + (unsigned)world - h % (unsigned)world) % (unsigned)world) != T->rank) return -1;
   if (T->layout == DT_OUT_SLAB) {
-    long long slot = tid / world;
     int px = (x - x0) % tw, py = (y - y0) % th;
     return ((slot * th + py) * tw + px) * 3;
   }

@@ -129,7 +129,31 @@ def test_tiles_partition_every_pixel_once(world):
     owner = img.reshape(g.yRes, g.xRes, 3)[::-1, :, 0] - 1   # back to y-up
     ty, tx = np.meshgrid(np.arange(g.yRes) // 16, np.arange(g.xRes) // 32, indexing="ij")
     tiles_x = (g.xRes + 31) // 32
-    assert np.array_equal(owner, (ty * tiles_x + tx) % world)
+    assert np.array_equal(owner, _tile_owner(ty * tiles_x + tx, world))
+
+
+def _tile_owner(tid, world):
+    """rank owning tile tid (dt_scene_dev.h tile_of: groups of `world` tiles, ranks rotated by a
+    hash of the group)"""
+    slot = (tid // world).astype(np.uint64)
+    h = (slot * 2654435761) & 0xffffffff
+    h ^= h >> 15
+    h = (h * 0x2c1b3c6d) & 0xffffffff
+    h ^= h >> 12
+    return ((tid % world) + world - (h % world).astype(np.int64)) % world
+
+
+def test_tile_split_balances_columns():
+    """At 1920 px (60 tiles a row) a plain t % 8 interleave gives ranks r and r+4 the same tile
+    columns; the hashed rotation spreads every rank over all columns."""
+    tiles_x, tiles_y, world = 60, 34, 8
+    tid = np.arange(tiles_x * tiles_y)
+    owner = _tile_owner(tid, world)
+    for r in range(world):
+        cols = np.bincount(tid[owner == r] % tiles_x, minlength=tiles_x)
+        assert (cols > 0).sum() >= 50            # t % 8: 15 columns per rank
+        assert ((tid % world == r) & (tid % tiles_x % 4 == r % 4)).sum() == (tid % world == r).sum()
+        assert abs(int((owner == r).sum()) - len(tid) / world) <= 1
 
 
 def test_oracle_center_pixel_anchor():

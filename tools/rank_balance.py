@@ -1,0 +1,48 @@
+"""Per-rank share of the tile split on ONE GPU: for world N in {1, 2, 4, 8}, render every rank's
+slab (the tiles t % N == r, DT_OUT_SLAB) one after another on this device and report each rank's
+trace-kernel time. With one GPU per rank the frame takes max_r T_r plus the gather, so
+T_1 / (N * max_r T_r) bounds the kernel-side strong-scaling efficiency of bench.py at N GPUs
+(load balance of the interleaved tiles, the persistent grid's tail on 1/N of the pixels).
+
+    python tools/rank_balance.py [c3|c2|c4] [reps]
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import distraytracer_amd as dt  # noqa: E402
+
+
+def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    g, built = bench.build_globals(dt, cfg)
+    scene = dt.Scene(built, g)
+    t1 = None
+    for world in (1, 2, 4, 8):
+        per, work = [], []
+        for rank in (range(world) if not os.environ.get("REVERSE") else reversed(range(world))):
+            tile = dt.tiles(rank=rank, world=world, layout=dt.DT_OUT_SLAB)
+            out = torch.zeros(max(dt.slab_floats(g, tile), 1), dtype=torch.float32, device="cuda")
+            st = dt.render(scene, g, 240, out, tile)   # warm-up
+            best = min(dt.render(scene, g, 240, out, tile).kernel_ms for _ in range(reps))
+            per.append(round(best, 3))
+            # work proxies: rays and shadow rays traced, in millions
+            work.append((round(st.rays / 1e6, 2), round(st.shadow_rays / 1e6, 2)))
+        if os.environ.get("REVERSE"):
+            per, work = per[::-1], work[::-1]
+        if world == 1:
+            t1 = per[0]
+        mx = max(per)
+        print(json.dumps({"config": cfg, "world": world, "kernel_ms_per_rank": per, "max_ms": mx,
+                          "mean_ms": round(sum(per) / world, 3),
+                          "kernel_efficiency": round(t1 / (world * mx), 4), "rays_shadow_M": work}), flush=True)
+    scene.close()
+
+
+if __name__ == "__main__":
+    main()
