@@ -21,6 +21,7 @@ extern "C" size_t dt_scene_struct_offset(void);
 extern "C" size_t dt_params_struct_offset(void);
 extern "C" hipError_t dt_launch_trace(const void* dev_launch, float* out, int grid, hipStream_t stream);
 extern "C" hipError_t dt_launch_sky(const void* dev_launch, float* out, int64_t n_threads, hipStream_t stream);
+extern "C" hipError_t dt_launch_sky_miss(const void* dev_launch, float* out, int64_t n_px, hipStream_t stream);
 extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_t slab_floats, const float* slabs,
                                        float* image, hipStream_t stream);
 extern "C" const void* dt_trace_kernel_ptr(void);
@@ -48,6 +49,7 @@ struct HScene {
   const int32_t* bparent;   // parent of every reference-tree node
   const uint32_t* pl_cells; // primary-ray candidate lists (host_primlists.cpp)
   const uint32_t* pl_list;
+  uint8_t* sky_miss;
 };
 
 #define DT_N_STAMPS (64 + 3 * 8 * 256)   // diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters):
@@ -132,6 +134,8 @@ struct dt_scene {
   std::vector<std::vector<P3>> fhull, bhull;   // leaf hull points per fast / bump tree node (host_hull.cpp)
   bool pl_bump = false;                        // lists for the blur passes follow the pass-0 lists
   std::vector<double> pl_key;
+  uint8_t* d_sky_miss = nullptr;   // 1-spp launches: missed-pixel flags (dt_sky_miss_kernel clears them)
+  int64_t sky_miss_cap = 0;
   PrimLists pl;
   bool pl_ok = false;
   void* d_pl_cells = nullptr;
@@ -270,7 +274,7 @@ void dt_scene_destroy(dt_scene* s)
 {
   if (!s) return;
   void* bufs[] = {s->d_pl_cells, s->d_pl_list, s->d_nodes, s->d_fnodes, s->d_bnodes, s->d_bparent, s->d_sg_cells, s->d_sg_list, s->d_leaf, s->d_hdr, s->d_geom, s->d_mat, s->d_lights, s->d_tex, s->d_zs,
-                  s->d_stats, s->d_launch};
+                  s->d_stats, s->d_launch, s->d_sky_miss};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -520,8 +524,27 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   // over ranks, where one such wave bounds a rank's kernel; DT_PRIO_STEPS=<n> overrides (0: off)
   static const char* ps = getenv("DT_PRIO_STEPS");
   PL.prio_steps = ps ? atoi(ps) : (PL.world > 1 ? 8 : 0);
+  // 1 spp (C5's cloud frames, n >= 244: nearly every pixel is sky): the trace kernel only flags
+  // the missed pixels and dt_sky_miss_kernel marches their sky one pixel per lane, instead of the
+  // wave marching each of its 64 pixels cooperatively in turn. DT_SKY_DEFER=0 disables it.
+  static const bool defer_on = !(getenv("DT_SKY_DEFER") && getenv("DT_SKY_DEFER")[0] == '0');
+  const int64_t n_px = PL.n_items * PL.ppw;
+  PL.sky_defer = 0;
+  hs.sky_miss = nullptr;
+  if (defer_on && PL.spp == 1 && PL.perlin_cloud && n_px > 0) {
+    if (n_px > sc->sky_miss_cap) {
+      HIPCHK(hipStreamSynchronize(st));
+      if (sc->d_sky_miss) (void)hipFree(sc->d_sky_miss);
+      sc->d_sky_miss = nullptr;
+      HIPCHK(hipMalloc((void**)&sc->d_sky_miss, n_px));
+      HIPCHK(hipMemsetAsync(sc->d_sky_miss, 0, n_px, st));
+      sc->sky_miss_cap = n_px;
+    }
+    PL.sky_defer = 1;
+    hs.sky_miss = sc->d_sky_miss;
+  }
   memset(sc->h_launch, 0, dt_launch_size());
-  memcpy(sc->h_launch + dt_scene_struct_offset(), &hs, sizeof(hs));
+  memcpy(sc->h_launch + dt_scene_struct_offset(), &hs, sizeof(hs));   // after every hs field is set
   memcpy(sc->h_launch + dt_params_struct_offset(), &PL, sizeof(PL));
   if (nz) HIPCHK(hipMemcpyAsync(sc->d_zs, sc->h_zs, nz * sizeof(float), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(sc->d_launch, sc->h_launch, dt_launch_size(), hipMemcpyHostToDevice, st));
@@ -530,6 +553,7 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 1 + DT_N_STAMPS), st));
   HIPCHK(hipEventRecord(sc->ev0, st));
   HIPCHK(dt_launch_trace(sc->d_launch, out_dev, (int)grid, st));
+  if (PL.sky_defer) HIPCHK(dt_launch_sky_miss(sc->d_launch, out_dev, n_px, st));
   HIPCHK(hipEventRecord(sc->ev1, st));
   sc->timed = true;
   sc->last = P;

@@ -126,6 +126,7 @@ struct DScene {
   const int32_t* bparent;   // parent of every reference node (-1: root)
   const uint32_t* pl_cells; // primary-ray candidate lists (host_primlists.cpp): (first, count) per pixel block
   const uint32_t* pl_list;  // (fast-tree node, float bits of t_near) per entry
+  uint8_t* sky_miss;        // P.sky_defer: per queue position, 1 when the pixel's sample missed
 };
 
 // pow(x, n) for the integer exponents the reference writes as pow(x, 2.0) etc. pow(x, 1) is x
@@ -316,7 +317,7 @@ __device__ V3 cloud_finish(const DParams& P, V3 color)
 }
 
 // full cloudColor on one lane
-__device__ V3 cloud_color_lane(const DParams& P, const float* __restrict__ zs, V3 ray)
+__device__ __forceinline__ V3 cloud_color_lane(const DParams& P, const float* __restrict__ zs, V3 ray)
 {
   V3 sky = sky_color(P, ray);
   V3 color = sky;
@@ -2234,8 +2235,11 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       DT_T(k1);
       DT_ACC(5, k0, k1);
       const bool miss = valid && !hit0;
-      // sky for missing samples: computed once per pixel by the whole wave
-      if (P.perlin_cloud) {
+      // sky for missing samples: computed once per pixel by the whole wave, or (1 spp,
+      // P.sky_defer) flagged for dt_sky_miss_kernel
+      if (P.sky_defer) {
+        if (miss) S.sky_miss[item * group + j] = 1;
+      } else if (P.perlin_cloud) {
         for (int jj = 0; jj < group; ++jj) {
           if (__ballot(miss && j == jj)) {
             int qx, qy;
@@ -2284,7 +2288,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       int64_t qo;
       bool qv;
       pixel_of(P, item * group + lane, qx, qy, qo, qv);
-      if (qv) {
+      if (qv && !(P.sky_defer && S.sky_miss[item * group + lane])) {
         V3 color = divs(v3(psum[0][lane], psum[1][lane], psum[2][lane]), spp);
 #ifdef DT_ITEM_TIMES   // diagnostic builds: the item's wave cycles / 1e4 in every channel
         color = v3(1, 1, 1);
@@ -2320,6 +2324,58 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       atomicAdd(S.stats + ST_TEX, tx);
     }
   }
+}
+
+// The sky of the pixels a 1-spp trace launch flagged as missed (P.sky_defer): renderImage's miss
+// branch (cpp:1074-1092: cloudColor of mcam * focalPoint) one pixel per lane, at the occupancy of a
+// small kernel instead of inside the trace kernel's register budget. With one sample the pixel is
+// that sample's colour (0 + c, then / 1: exact), so the store is the trace kernel's. Clears the flags.
+extern "C" __global__ void __launch_bounds__(256)
+dt_sky_miss_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
+{
+  const DParams& P = Lp->P;
+  const DScene& S = Lp->S;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool mine = q < P.n_items * P.ppw && S.sky_miss[q];
+  if (mine) {
+    S.sky_miss[q] = 0;
+    int x, y;
+    int64_t so;
+    bool valid;
+    pixel_of(P, q, x, y, so, valid);
+    const V3 eye = v3a(P.eye), X = v3a(P.X), Y = v3a(P.Y), Z = v3a(P.Z);
+    float aa = P.l + (P.r - P.l) * (float)x / (float)P.xRes;
+    float bb = P.b + (P.t - P.b) * (float)y / (float)P.yRes;
+    V3 rd = sub(add(mul(aa, X), mul(bb, Y)), mul(P.near_plane, Z));
+    V3 fp = add(eye, mul(P.focal_length, rd));
+    V3 pt;
+    pt.x = ((P.sky_m[0][0] * fp.x + P.sky_m[0][1] * fp.y) + P.sky_m[0][2] * fp.z) + P.sky_m[0][3] * 1.0;
+    pt.y = ((P.sky_m[1][0] * fp.x + P.sky_m[1][1] * fp.y) + P.sky_m[1][2] * fp.z) + P.sky_m[1][3] * 1.0;
+    pt.z = ((P.sky_m[2][0] * fp.x + P.sky_m[2][1] * fp.y) + P.sky_m[2][2] * fp.z) + P.sky_m[2][3] * 1.0;
+#ifdef DT_SKYMISS_DEBUG   // diagnostic builds: the march input point, raw
+    if (valid) {
+      const int64_t off = P.layout == DT_OUT_SLAB ? so : 3 * ((int64_t)(P.yRes - 1 - y) * P.xRes + x);
+      const V3 sk = sky_color(P, pt);
+      int nd = 0;
+      float dsum = 0;
+      for (int k = 0; k < P.n_cloud_steps; ++k) {
+        const float d = cloud_step(P, S.cloud_z[k], pt);
+        if (d >= 0.0f) { ++nd; dsum += d; }
+      }
+      out[off] = (float)sk.x; out[off + 1] = (float)nd; out[off + 2] = dsum;
+    }
+    if (false)
+#endif
+    {
+    const V3 color = cloud_color_lane(P, S.cloud_z, pt);
+    if (valid) {
+      store_pixel(P, out, x, y, so, color);
+      if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
+    }
+    }
+  }
+  const unsigned long long n = __popcll(__ballot(mine));
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(S.stats + ST_SKY, n);
 }
 
 // renderImageCloud (cpp:1224-1279): one pixel per lane
@@ -2386,6 +2442,12 @@ extern "C" size_t dt_params_struct_offset(void) { return offsetof(DLaunch, P); }
 extern "C" hipError_t dt_launch_trace(const void* dev_launch, float* out, int grid, hipStream_t stream)
 {
   hipLaunchKernelGGL(dt_trace_kernel, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
+  return hipGetLastError();
+}
+extern "C" hipError_t dt_launch_sky_miss(const void* dev_launch, float* out, int64_t n_px, hipStream_t stream)
+{
+  int64_t blocks = (n_px + 255) / 256;
+  hipLaunchKernelGGL(dt_sky_miss_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const DLaunch*)dev_launch, out);
   return hipGetLastError();
 }
 extern "C" hipError_t dt_launch_sky(const void* dev_launch, float* out, int64_t n_threads, hipStream_t stream)
