@@ -728,7 +728,7 @@ __device__ bool shape_shadow(int type, uint32_t flags, GP g, V3 ray, V3 start,
 }
 
 // GeoPrimitive::getNorm (per-lane shape index)
-__device__ V3 shape_norm(int type, uint32_t flags, GP g, V3 p, float shift,
+__device__ __forceinline__ V3 shape_norm(int type, uint32_t flags, GP g, V3 p, float shift,
                          unsigned long long* st_prism)
 {
   switch (type) {
@@ -780,7 +780,7 @@ __device__ V3 shape_norm(int type, uint32_t flags, GP g, V3 p, float shift,
 }
 
 // GeoPrimitive::getUV (type 0/1/2)
-__device__ int shape_uv(int type, uint32_t flags, GP g, V3 p, float shift,
+__device__ __forceinline__ int shape_uv(int type, uint32_t flags, GP g, V3 p, float shift,
                         double& uo, double& vo)
 {
   switch (type) {
@@ -1543,7 +1543,7 @@ __device__ __forceinline__ bool is_refl_material(int m)
 }
 
 // glossy sample rectangle (cpp:648-669 / 742-755)
-__device__ void glossy_rect(V3 refl_ray, V3 isectP, float mult, V3& A, V3& B, V3& C, V3& D, V3& wv, V3& lv)
+__device__ __forceinline__ void glossy_rect(V3 refl_ray, V3 isectP, float mult, V3& A, V3& B, V3& C, V3& D, V3& wv, V3& lv)
 {
   const float length = 1, width = 0.5;
   V3 gloss_ray = mul(mult, refl_ray);
