@@ -1245,6 +1245,9 @@ __device__ __forceinline__ void shadow_leaf(const DScene& S, const DNodeDev& nd,
     leaf_shape(S, nd, q, sid, type, flags, off);
     DT_CNT(8);
     DT_CNT(18 + (type & 7));   // shadow prim tests by type (8 -> 18)
+#ifdef DT_STAMPS
+    cnt.ph[42 + cnt.cur_path] += 1;   // wave-level shadow prim tests by path
+#endif
     const bool test = hb && !occl && sid != skip_shape;
 #ifdef DT_STAMPS
     const unsigned long long occ_before = __ballot(occl);
@@ -1415,6 +1418,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
                                          V3 sstart, float t_max, int skip_shape, int li, float shift, CNT& cnt)
 {
   const Walk w = make_walk(P, active, sray, bstart, shift);
+#ifdef DT_STAMPS
+  cnt.cur_path = 2;
+#endif
   if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift)))
     return occluded_walk<1>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
   // blur passes use the grid when its lists were built for their shifts (sg_ypad)
@@ -1453,6 +1459,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       if (off & DT_SG_UMBRA) return true;   // every segment of the cell crosses one face (host_shadowgrid.cpp)
       if (n != DT_SG_WALK) {
         DT_CNT(35);
+#ifdef DT_STAMPS
+        cnt.cur_path = 0;
+#endif
         return bump_list ? occluded_list<true>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, off, n, cnt)
                          : occluded_list<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, off, n, cnt);
       }
@@ -1480,6 +1489,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       // too long) walk the tree afterwards, unless the union already occluded them all
       if (__ballot(active && lin)) {
         DT_CNT(41);
+#ifdef DT_STAMPS
+        cnt.cur_path = 1;
+#endif
         const bool o = bump_list ? occluded_union<true>(S, w, active && lin, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt)
                                  : occluded_union<false>(S, w, active && lin, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
         if (!out_lanes) return o;
@@ -1489,6 +1501,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
 #else
       if (!out_lanes) {
         DT_CNT(41);
+#ifdef DT_STAMPS
+        cnt.cur_path = 1;
+#endif
         return bump_list ? occluded_union<true>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt)
                          : occluded_union<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
       }
@@ -1496,6 +1511,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
     }
 #endif
   }
+#ifdef DT_STAMPS
+  cnt.cur_path = 2;
+#endif
   if (w.bump_wave) return occ_union | occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
   return occ_union | occluded_walk<0>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 }
@@ -1527,6 +1545,7 @@ struct Counters {
 #ifdef DT_STAMPS
   unsigned long long ph[64];   // diagnostic build only: cycles per phase, event counts (wave-uniform)
   int cur_li;                  // light of the current shadow test (per-shape histogram)
+  int cur_path;                // shadow path of the current test: 0 cell list, 1 union, 2 tree walk
 #endif
 };
 
@@ -2153,6 +2172,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
 #ifdef DT_STAMPS
   for (int k = 0; k < 64; ++k) cnt.ph[k] = 0;
   cnt.cur_li = 0;
+  cnt.cur_path = 0;
 #endif
 
   int64_t item = 0, batch_end = 0;
