@@ -408,7 +408,10 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
     P.sg_lo[a] = sc->sg.lo[a];
     P.sg_inv[a] = sc->sg.inv_h[a];
   }
-  for (int l = 0; l < DT_MAX_SGRID; ++l) P.sg_base[l] = sc->sg.base[l];
+  for (int l = 0; l < DT_MAX_SGRID; ++l) {
+    P.sg_base[l] = sc->sg.base[l];
+    P.sg_base0[l] = sc->sg.base0[l];
+  }
   P.sg_reach = sc->sg.reach;
   P.sg_ypad = (float)sc->sg.ypad;
 
@@ -522,12 +525,12 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   PL.item_batch = PL.n_items >= 64 * grid ? 2 : 1;
   // deep-cascade waves raise their priority (dt_kernels.hip, DT_PRIO_STEPS) when the frame is split
   // over ranks, where one such wave bounds a rank's kernel; DT_PRIO_STEPS=<n> overrides (0: off)
-  static const char* ps = getenv("DT_PRIO_STEPS");
+  const char* ps = getenv("DT_PRIO_STEPS");
   PL.prio_steps = ps ? atoi(ps) : (PL.world > 1 ? 8 : 0);
   // 1 spp (C5's cloud frames, n >= 244: nearly every pixel is sky): the trace kernel only flags
   // the missed pixels and dt_sky_miss_kernel marches their sky one pixel per lane, instead of the
   // wave marching each of its 64 pixels cooperatively in turn. DT_SKY_DEFER=0 disables it.
-  static const bool defer_on = !(getenv("DT_SKY_DEFER") && getenv("DT_SKY_DEFER")[0] == '0');
+  const bool defer_on = !(getenv("DT_SKY_DEFER") && getenv("DT_SKY_DEFER")[0] == '0');
   const int64_t n_px = PL.n_items * PL.ppw;
   PL.sky_defer = 0;
   hs.sky_miss = nullptr;

@@ -1437,7 +1437,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   // Measured slower for scattered waves: per-lane list walks with a per-lane shape switch (C3 1725
   // vs 1932, C4 843 vs 936 Mpixel-samples/s), the lists of two cells in turn.
   bool occ_union = false;   // DT_SG_MIXED: lanes answered by the union walk
-  if (li < P.sg_n && P.sg_base[li] >= 0) {
+  // blur passes use the padded lists, pass-0 rays the unpadded ones when a second grid was built
+  const int sg_b = w.bump_wave ? P.sg_base[li] : P.sg_base0[li];
+  if (li < P.sg_n && sg_b >= 0) {
     const unsigned long long am = __ballot(active);
     if (!am) return false;
     float x, y, z;
@@ -1454,7 +1456,7 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
     DT_CNT(inside ? 36 : 38);
     if (DT_SG_COHERENT && inside && !__ballot(active & !near)) {
       const int c0 = ((int)z0 * P.sg_dim[1] + (int)y0) * P.sg_dim[0] + (int)x0;
-      const DT_CAS uint32_t* e = cas(S.sg_cells) + 2 * (size_t)(P.sg_base[li] + c0);
+      const DT_CAS uint32_t* e = cas(S.sg_cells) + 2 * (size_t)(sg_b + c0);
       const uint32_t off = e[0], n = e[1];
       if (off & DT_SG_UMBRA) return true;   // every segment of the cell crosses one face (host_shadowgrid.cpp)
       if (n != DT_SG_WALK) {
@@ -1475,7 +1477,7 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       uint32_t loff = 0, ln = 0;
       if (active && lin) {
         const int cl = ((int)fz * P.sg_dim[1] + (int)fy) * P.sg_dim[0] + (int)fx;
-        const uint2 e = ((const uint2*)S.sg_cells)[(size_t)P.sg_base[li] + cl];
+        const uint2 e = ((const uint2*)S.sg_cells)[(size_t)sg_b + cl];
         loff = e.x;
         ln = e.y;
         lin = ln != DT_SG_WALK;

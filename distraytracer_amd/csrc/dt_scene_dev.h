@@ -119,6 +119,7 @@ struct DParams {
   int32_t sg_n;           // shadow grid: lights 0..sg_n-1 (sg_base < 0: none for that light)
   int32_t sg_dim[3];
   int32_t sg_base[DT_MAX_SGRID];
+  int32_t sg_base0[DT_MAX_SGRID];   // pass-0 rays (no shift): the unpadded grid when one was built
   float sg_lo[3], sg_inv[3];
   float sg_reach;         // a cell's list also covers points this many cells outside it
   float sg_ypad;          // the lists also hold for blur passes whose |shift| <= sg_ypad

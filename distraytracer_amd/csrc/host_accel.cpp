@@ -102,6 +102,31 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
       !build_shadow_grid(dnodes, f, a.sg, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : 0.5f,
                          a.n_bnodes > 0 ? (double)a.bump_pad : 0.0))
     a.sg = ShadowGrid();
+  for (int l = 0; l < DT_MAX_SGRID; ++l) a.sg.base0[l] = a.sg.base[l];
+  // Large blur shifts pad the lists until most cells overflow and walk the tree, pass-0 rays
+  // included (C5 frames 1760-1920: 45-70% of the cells). Then an unpadded grid for the pass-0 rays
+  // goes after it in the same pools (same cells, other lists; 0-5% of its cells walk).
+  // DT_SG_PASS0: 0 never, 1 whenever the lists are padded, default when > 10% of cells walk.
+  if (a.sg.ypad > 0 && !a.sg.cells.empty()) {
+    size_t walk = 0, cells = a.sg.cells.size() / 2;
+    for (size_t c = 0; c < cells; ++c) walk += a.sg.cells[2 * c + 1] == DT_SG_WALK;
+    const char* p0 = getenv("DT_SG_PASS0");
+    const bool want = p0 ? p0[0] == '1' : walk > cells / 10;
+    ShadowGrid g0;
+    if (want && build_shadow_grid(dnodes, f, g0, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : 0.5f, 0.0) &&
+        g0.n_lights == a.sg.n_lights && g0.dim[0] == a.sg.dim[0] && g0.dim[1] == a.sg.dim[1] && g0.dim[2] == a.sg.dim[2]) {
+      const uint32_t cell_off = (uint32_t)(a.sg.cells.size() / 2), list_off = (uint32_t)a.sg.list.size();
+      for (size_t c = 0; c < g0.cells.size(); c += 2) {
+        uint32_t o = g0.cells[c];
+        if (g0.cells[c + 1] != DT_SG_WALK) o = (o & DT_SG_UMBRA) | ((o & ~DT_SG_UMBRA) + list_off);
+        a.sg.cells.push_back(o);
+        a.sg.cells.push_back(g0.cells[c + 1]);
+      }
+      a.sg.list.insert(a.sg.list.end(), g0.list.begin(), g0.list.end());
+      for (int l = 0; l < DT_MAX_SGRID; ++l) a.sg.base0[l] = g0.base[l] >= 0 ? g0.base[l] + (int32_t)cell_off : -1;
+      a.sg.umbra_cells += g0.umbra_cells;
+    }
+  }
   if (getenv("DT_SG_VERBOSE")) {
     size_t cells = a.sg.cells.size() / 2, tree = 0, sum = 0, mx = 0;
     for (size_t c = 0; c < cells; ++c) {

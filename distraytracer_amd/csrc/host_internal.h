@@ -33,6 +33,8 @@ std::vector<int32_t> tree_parents(const std::vector<dtd::DNodeDev>& ref);
 struct ShadowGrid {
   int n_lights = 0;                  // lights 0..n_lights-1 (base[l] < 0: that light has none)
   int32_t base[DT_MAX_SGRID] = {};   // first cell record of light l in `cells`
+  int32_t base0[DT_MAX_SGRID] = {};  // the same for pass-0 (unshifted) rays: `base`, or an unpadded
+                                     // second grid appended to `cells` / `list` (host_accel.cpp)
   int dim[3] = {0, 0, 0};
   float lo[3] = {0, 0, 0}, inv_h[3] = {0, 0, 0};
   float reach = 0.5f;                // a cell's list covers points this many cells outside it

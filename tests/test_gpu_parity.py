@@ -157,9 +157,12 @@ def test_final_c5_tunnel_motion_blur(cuda, n):
     _cmp(gpu[m], ref[m], 0.003, "final C5 frame %d" % (n * 8))
 
 
-def test_final_c5_cloud_frame(cuda):
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_final_c5_cloud_frame(cuda, monkeypatch, defer):
     """C5 cloud frame buildFinal(2000) (n = 250 >= 244): the builder forces 1 spp and no aperture
-    (scene.h:795-796); 64 pixels per wave, each missing pixel's sky marched cooperatively."""
+    (scene.h:795-796); 64 pixels per wave. The missed pixels' sky is marched per lane by
+    dt_sky_miss_kernel (default), or cooperatively by the wave (DT_SKY_DEFER=0)."""
+    monkeypatch.setenv("DT_SKY_DEFER", defer)
     g = dt.globals_default()
     g.use_model = 0
     built = dt.build_scene("final", 2000, g)
@@ -276,6 +279,28 @@ def test_shadow_grid_hull_culling_tunnel(cuda, monkeypatch, frame):
     monkeypatch.setenv("DT_SHADOW_GRID", "1")
     for mode in ("0", "1", "2"):
         monkeypatch.setenv("DT_SG_HULL", mode)
+        img, st = _render_gpu(built, g, frame, tile)
+        assert st.shadow_rays == ref_st.shadow_rays, mode
+        assert np.array_equal(img, ref_img), mode
+
+
+@pytest.mark.parametrize("frame", [1680, 1920])
+def test_shadow_grid_pass0_lists(cuda, monkeypatch, frame):
+    """Large blur shifts: an unpadded second grid serves the pass-0 rays while the blur passes
+    keep the padded lists or walk (host_accel.cpp, DT_SG_PASS0). Tunnel windows at frames 1680
+    (shift <= 5) and 1920 (<= 81) with it forced on and off must match tree walks bit for bit."""
+    g = dt.globals_default()
+    g.use_model = 0
+    built = dt.build_scene("final", frame, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = 480, 270, 16, 10
+    tile = dt.tiles(x0=160, y0=80, x1=320, y1=176)
+    for k in ("DT_SG_CELLS", "DT_SG_REACH", "DT_SG_BLOCK", "DT_SG_ORDER", "DT_SG_HULL", "DT_SG_PASS0"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("DT_SHADOW_GRID", "0")
+    ref_img, ref_st = _render_gpu(built, g, frame, tile)
+    monkeypatch.setenv("DT_SHADOW_GRID", "1")
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DT_SG_PASS0", mode)
         img, st = _render_gpu(built, g, frame, tile)
         assert st.shadow_rays == ref_st.shadow_rays, mode
         assert np.array_equal(img, ref_img), mode

@@ -182,12 +182,29 @@ def test_oracle_sky_image_cloud_anchor():
 def _accel(name, frame, models, env, monkeypatch):
     for k in ("DT_SG_BLOCK", "DT_SG_ORDER", "DT_SG_HULL", "DT_SG_UMBRA"):
         monkeypatch.delenv(k, raising=False)
+    # the padded grid alone (its walk-cell share decides whether a pass-0 grid is appended)
+    monkeypatch.setenv("DT_SG_PASS0", "0")
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     g = dt.globals_default()
     g.use_model = models
     b = dt.build_scene("final", frame, g)
     return dt.accel_info(b, g)
+
+
+def test_shadow_grid_pass0_grid_appended(monkeypatch):
+    """Frame 1920's blur shifts (<= 81) pad the lists until most cells walk; the pass-0 grid is
+    appended (same cells, unpadded lists) and walks almost nowhere."""
+    pad = _accel("c5-1920", 1920, 0, {}, monkeypatch)
+    both = _accel("c5-1920", 1920, 0, {"DT_SG_PASS0": "1"}, monkeypatch)
+    assert pad["sg_tree_cells"] > pad["sg_cells"] // 4
+    assert both["sg_cells"] == 2 * pad["sg_cells"]
+    assert both["sg_tree_cells"] - pad["sg_tree_cells"] < pad["sg_cells"] // 20
+    monkeypatch.delenv("DT_SG_PASS0")
+    g = dt.globals_default()
+    g.use_model = 0
+    dflt = dt.accel_info(dt.build_scene("final", 1920, g), g)
+    assert dflt["sg_cells"] == both["sg_cells"]
 
 
 # C3's room, C4's meshes (2442 leaves), a C5 tunnel frame with blur-padded lists
