@@ -86,7 +86,11 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
     const double pad = (((double)fabsf(g.move_per_frame) * d + (double)fabsf(g.accel_t) * d * d * d) * 1.01 + 1e-6) *
                        (bps ? atof(bps) : 1.0);
     a.bump_pad = (float)pad;
-    if (!(bt && bt[0] == '0') && g.blur_samples > 0 && pad > 0 && pad < 1e3 && build_fast_tree(dnodes, a.bnodes, pad, eye))
+    // every shift is >= 0 when move_per_frame, accel_t and frame_range are (cpp:1101-1111):
+    // planar leaves then need no padding below (DT_BUMP_UP=0: the symmetric +-pad of round 1)
+    const char* bu = getenv("DT_BUMP_UP");
+    const bool up_only = !(bu && bu[0] == '0') && g.move_per_frame >= 0 && g.accel_t >= 0 && g.frame_range >= 0;
+    if (!(bt && bt[0] == '0') && g.blur_samples > 0 && pad > 0 && pad < 1e3 && build_fast_tree(dnodes, a.bnodes, pad, eye, up_only))
       a.n_bnodes = (int)a.bnodes.size();
     else
       a.bnodes.clear();

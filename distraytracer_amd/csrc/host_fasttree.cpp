@@ -152,7 +152,7 @@ struct Builder {
 // ref: the reference tree in device format (pre-order, last child first, skip links).
 // Returns false (and leaves `out` empty) when the tree cannot carry 16-bit leaf ranks.
 bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNodeDev>& out, double ypad,
-                     const double* eye)
+                     const double* eye, bool up_only)
 {
   out.clear();
   Builder b(ref, ypad, eye);
@@ -165,8 +165,25 @@ bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNo
       L.c[a] = 0.5 * (L.lb[a] + L.ub[a]);
     }
     if (ypad > 0) {
-      L.lb[1] = L.lb[1] - ypad;
-      L.ub[1] = L.ub[1] + ypad;
+      // The leaf box only filters the walk (the device decides the reference's gather exactly at
+      // the leaf, bump_leaf_gathered) and bounds its culling, so it must hold every point the
+      // leaf's shapes can be hit at. Spheres and cylinders, and leaves of several shapes: the
+      // bumped box at the largest shift, +-ypad. With non-negative shifts (up_only) a planar
+      // shape's hits lie on it up to the rounding of its float tests, far inside the 1e-2 leaf
+      // padding (the argument of the shadow grid's hull culling): a moving "rectangle" within
+      // [lb, ub + ypad], any other planar shape within [lb, ub].
+      double lo_pad = ypad, hi_pad = ypad;
+      if (up_only && (ref[i].meta & dtd::DN_SINGLE)) {
+        const int type = (int)((ref[i].meta >> 4) & 15u);
+        const uint32_t flags = (ref[i].meta >> 8) & 0xffu;
+        if (type == DT_SHAPE_TRIANGLE || type == DT_SHAPE_RECTANGLE || type == DT_SHAPE_RECTPRISM_V2 ||
+            type == DT_SHAPE_CHECKERBOARD || type == DT_SHAPE_CHECKERBOARD_HOLE) {
+          lo_pad = 0;
+          hi_pad = (flags & DT_F_NAMED_RECT) ? ypad : 0;
+        }
+      }
+      L.lb[1] = L.lb[1] - lo_pad;
+      L.ub[1] = L.ub[1] + hi_pad;
       if (!(L.lb[1] <= L.ub[1])) return false;
     }
     L.node = (int)i;

@@ -24,8 +24,10 @@ void build_bvh(const dt_scene_desc& d, const dt_globals& g, FlatBVH& out);
 // host_fasttree.cpp: same leaves, SAH inner nodes, 16-bit leaf ranks in meta (false: no fast tree)
 // ypad > 0: the motion-blur bump tree (leaf y-bounds padded, leaf skip = reference node index)
 // eye: children ordered nearer-to-eye first (null: SAH order); the gathered set never depends on it
+// up_only: every blur shift is >= 0, so single-shape planar leaves are padded by what their shape
+// can reach (host_fasttree.cpp) instead of +-ypad
 bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNodeDev>& out, double ypad = 0,
-                     const double* eye = nullptr);
+                     const double* eye = nullptr, bool up_only = false);
 // parent of every node of a pre-order skip-link tree (-1 at the root)
 std::vector<int32_t> tree_parents(const std::vector<dtd::DNodeDev>& ref);
 

@@ -344,14 +344,15 @@ def test_primary_lists_match_tree_walks(cuda, monkeypatch, case):
         assert np.array_equal(img, ref_img), env
 
 
-@pytest.mark.parametrize("n", [150, 210])
+@pytest.mark.parametrize("n", [150, 210, 240])
 def test_bump_tree_matches_reference_walks(cuda, monkeypatch, n):
     """Motion-blur passes on the bump tree (host_fasttree.cpp: padded leaves, exact per-leaf
     bumped gather with the ancestor chain) and on the blur-padded shadow-grid lists must give the
     image of reference-tree walks bit for bit. Frame 1200 shifts by < 0.04, frame 1680 by up to 5
     (bumped leaf boxes outgrow their parents: the ancestor-chain test). DT_BUMP_PAD_SCALE=0.5
     pads for half the largest shift, so lanes beyond it send their waves to the reference walk.
-    Children order (DT_EYE_ORDER) must not matter either."""
+    Children order (DT_EYE_ORDER) must not matter either, nor the planar leaves' one-sided padding
+    (DT_BUMP_UP=0: +-pad on every leaf). Frame 1920 shifts by up to 81."""
     g = dt.globals_default()
     g.use_model = 0
     built = dt.build_scene("final", n * 8, g)
@@ -362,8 +363,8 @@ def test_bump_tree_matches_reference_walks(cuda, monkeypatch, n):
     monkeypatch.setenv("DT_FAST_TREE", "0")
     ref_img, ref_st = _render_gpu(built, g, n * 8, tile)
     assert ref_st.rays > ref_st.samples   # blur passes ran
-    for env in ({}, {"DT_BUMP_PAD_SCALE": "0.5"}, {"DT_EYE_ORDER": "0"}):
-        for k in ("DT_BUMP_TREE", "DT_SHADOW_GRID", "DT_FAST_TREE", "DT_BUMP_PAD_SCALE", "DT_EYE_ORDER"):
+    for env in ({}, {"DT_BUMP_PAD_SCALE": "0.5"}, {"DT_EYE_ORDER": "0"}, {"DT_BUMP_UP": "0"}):
+        for k in ("DT_BUMP_TREE", "DT_SHADOW_GRID", "DT_FAST_TREE", "DT_BUMP_PAD_SCALE", "DT_EYE_ORDER", "DT_BUMP_UP"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
