@@ -78,6 +78,10 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
   // margin for the float evaluation). The device checks every lane's shift against the pad and
   // walks the reference tree when one exceeds it. DT_BUMP_TREE=0 disables it.
   a.bparent = tree_parents(dnodes);
+  // every blur shift is >= 0 when move_per_frame, accel_t and frame_range are (cpp:1101-1111):
+  // planar leaves then need no padding below (blur_leaf_pad; DT_BUMP_UP=0: +-pad everywhere)
+  const char* bu = getenv("DT_BUMP_UP");
+  const bool up_only = !(bu && bu[0] == '0') && g.move_per_frame >= 0 && g.accel_t >= 0 && g.frame_range >= 0;
   {
     const char* bt = getenv("DT_BUMP_TREE");
     const double d = fabs((double)g.frame_range) * (1.0 + 1e-3) + 1e-3;
@@ -88,8 +92,7 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
     a.bump_pad = (float)pad;
     // every shift is >= 0 when move_per_frame, accel_t and frame_range are (cpp:1101-1111):
     // planar leaves then need no padding below (DT_BUMP_UP=0: the symmetric +-pad of round 1)
-    const char* bu = getenv("DT_BUMP_UP");
-    const bool up_only = !(bu && bu[0] == '0') && g.move_per_frame >= 0 && g.accel_t >= 0 && g.frame_range >= 0;
+
     if (!(bt && bt[0] == '0') && g.blur_samples > 0 && pad > 0 && pad < 1e3 && build_fast_tree(dnodes, a.bnodes, pad, eye, up_only))
       a.n_bnodes = (int)a.bnodes.size();
     else
@@ -104,7 +107,7 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
   const char* sgr = getenv("DT_SG_REACH");
   if ((sgv && sgv[0] == '0') ||
       !build_shadow_grid(dnodes, f, a.sg, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : 0.5f,
-                         a.n_bnodes > 0 ? (double)a.bump_pad : 0.0))
+                         a.n_bnodes > 0 ? (double)a.bump_pad : 0.0, up_only))
     a.sg = ShadowGrid();
   for (int l = 0; l < DT_MAX_SGRID; ++l) a.sg.base0[l] = a.sg.base[l];
   // Large blur shifts pad the lists until most cells overflow and walk the tree, pass-0 rays

@@ -172,16 +172,8 @@ bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNo
       // shape's hits lie on it up to the rounding of its float tests, far inside the 1e-2 leaf
       // padding (the argument of the shadow grid's hull culling): a moving "rectangle" within
       // [lb, ub + ypad], any other planar shape within [lb, ub].
-      double lo_pad = ypad, hi_pad = ypad;
-      if (up_only && (ref[i].meta & dtd::DN_SINGLE)) {
-        const int type = (int)((ref[i].meta >> 4) & 15u);
-        const uint32_t flags = (ref[i].meta >> 8) & 0xffu;
-        if (type == DT_SHAPE_TRIANGLE || type == DT_SHAPE_RECTANGLE || type == DT_SHAPE_RECTPRISM_V2 ||
-            type == DT_SHAPE_CHECKERBOARD || type == DT_SHAPE_CHECKERBOARD_HOLE) {
-          lo_pad = 0;
-          hi_pad = (flags & DT_F_NAMED_RECT) ? ypad : 0;
-        }
-      }
+      double lo_pad, hi_pad;
+      blur_leaf_pad(ref[i], ypad, up_only, lo_pad, hi_pad);
       L.lb[1] = L.lb[1] - lo_pad;
       L.ub[1] = L.ub[1] + hi_pad;
       if (!(L.lb[1] <= L.ub[1])) return false;

@@ -64,8 +64,25 @@ double hull_gap(const P3* A, int na, const P3* B, int nb, const P3& v);
 // `hint`: a direction tried first, returned as the one GJK ended with)
 bool hulls_separated(const P3* A, int na, const P3* B, int nb, double margin, P3& hint);
 
+// Blur passes: how far below / above its box a reference leaf's shapes can be hit at any shift
+// the frame draws (|shift| <= ypad): +-ypad for spheres, cylinders and leaves of several shapes
+// (the bumped box); with non-negative shifts (up_only) a single planar shape is hit on itself up to
+// the rounding of its float tests, far inside the 1e-2 leaf padding: [0, ypad] for a moving
+// "rectangle", nothing for any other.
+inline void blur_leaf_pad(const dtd::DNodeDev& n, double ypad, bool up_only, double& below, double& above)
+{
+  below = above = ypad;
+  if (!up_only || !(n.meta & dtd::DN_SINGLE)) return;
+  const int type = (int)((n.meta >> 4) & 15u);
+  const uint32_t flags = (n.meta >> 8) & 0xffu;
+  if (type == DT_SHAPE_TRIANGLE || type == DT_SHAPE_RECTANGLE || type == DT_SHAPE_RECTPRISM_V2 ||
+      type == DT_SHAPE_CHECKERBOARD || type == DT_SHAPE_CHECKERBOARD_HOLE) {
+    below = 0;
+    above = (flags & DT_F_NAMED_RECT) ? ypad : 0;
+  }
+}
 bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene& fs, ShadowGrid& g,
-                       double target_cells = 32768, float reach = 0.5f, double ypad = 0);
+                       double target_cells = 32768, float reach = 0.5f, double ypad = 0, bool up_only = false);
 
 // device-layout scene produced from a descriptor (host_flatten.cpp)
 struct FlatScene {

@@ -203,7 +203,7 @@ bool shape_separated(const dtd::DShapeHdr& h, const double* g, const double clo[
 }  // namespace
 
 bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene& fs, ShadowGrid& g,
-                       double target_cells, float reach, double ypad)
+                       double target_cells, float reach, double ypad, bool up_only)
 {
   const double t_entry = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
   const std::vector<dtd::DLight>& lights = fs.lights;
@@ -274,13 +274,16 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   const double m1 = (reach + 0.05) * std::max({hh[0], hh[1], hh[2]}) + 1e-4 * (1 + scale);
   const double m2 = 2e-3 + 1e-4 * (1 + scale);
   const double mplane = 1e-3 + 1e-6 * (1 + scale);
-  // leaf boxes, padded by ypad in y for the blur passes' bumped boxes
+  // leaf boxes, padded in y by where the blur passes can hit their shapes (blur_leaf_pad)
   std::vector<std::array<double, 6>> lbox(nodes.size());
-  for (int leaf : leaves)
+  for (int leaf : leaves) {
+    double below = 0, above = 0;
+    if (ypad > 0) blur_leaf_pad(nodes[leaf], ypad, up_only, below, above);
     for (int a = 0; a < 3; ++a) {
-      lbox[leaf][a] = nodes[leaf].lb[a] - (a == 1 ? ypad : 0.0);
-      lbox[leaf][3 + a] = nodes[leaf].ub[a] + (a == 1 ? ypad : 0.0);
+      lbox[leaf][a] = nodes[leaf].lb[a] - (a == 1 ? below : 0.0);
+      lbox[leaf][3 + a] = nodes[leaf].ub[a] + (a == 1 ? above : 0.0);
     }
+  }
   // shapes of each leaf (shape ids)
   auto leaf_shapes = [&](int leaf, std::vector<int>& out) {
     out.clear();
