@@ -244,7 +244,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
     for (int i = 0; i < s->n_fnodes; ++i)
       if (s->fnodes_host[i].meta & dtd::DN_LEAF) leaf_hull_points(f, s->fnodes_host[i], -1, 0.0, s->fhull[i]);
     for (int i = 0; i < s->n_bnodes; ++i)
-      if (s->bnodes_host[i].meta & dtd::DN_LEAF) leaf_hull_points(f, s->bnodes_host[i], -1, (double)s->bump_pad, s->bhull[i]);
+      if (s->bnodes_host[i].meta & dtd::DN_LEAF) leaf_hull_points(f, s->bnodes_host[i], -1, (double)s->bump_pad, s->bhull[i], acc.bump_up_only);
   }
   if ((rc = upload(s->sg.cells, &s->d_sg_cells)) || (rc = upload(s->sg.list, &s->d_sg_list))) {
     dt_scene_destroy(s);

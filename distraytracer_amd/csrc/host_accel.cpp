@@ -82,6 +82,7 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
   // planar leaves then need no padding below (blur_leaf_pad; DT_BUMP_UP=0: +-pad everywhere)
   const char* bu = getenv("DT_BUMP_UP");
   const bool up_only = !(bu && bu[0] == '0') && g.move_per_frame >= 0 && g.accel_t >= 0 && g.frame_range >= 0;
+  a.bump_up_only = up_only;
   {
     const char* bt = getenv("DT_BUMP_TREE");
     const double d = fabs((double)g.frame_range) * (1.0 + 1e-3) + 1e-3;

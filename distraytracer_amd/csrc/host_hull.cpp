@@ -14,7 +14,8 @@ namespace dth {
 // corners of rectangle / checkerboard / prism-face tests, triangle vertices. A moving named
 // rectangle (blur passes, |shift| <= ypad in y) adds its shifted corners. false: no planar hull
 // (spheres, cylinders).
-bool shape_hull_points(const dtd::DShapeHdr& h, const double* g, double ypad, std::vector<std::array<double, 3>>& pts)
+bool shape_hull_points(const dtd::DShapeHdr& h, const double* g, double ypad, std::vector<std::array<double, 3>>& pts,
+                       bool up_only)
 {
   auto para = [&](const double* R, double yp) {
     for (int k = 0; k < 4; ++k) {
@@ -38,8 +39,8 @@ bool shape_hull_points(const dtd::DShapeHdr& h, const double* g, double ypad, st
         const double* D = g + dtd::RC_D;
         const double q[4][3] = {{A[0], A[1], A[2]}, {B[0], B[1], B[2]}, {D[0], D[1], D[2]},
                                 {B[0] + D[0] - A[0], B[1] + D[1] - A[1], B[2] + D[2] - A[2]}};
-        for (const auto& p : q) {
-          pts.push_back({p[0], p[1] - ypad, p[2]});
+        for (const auto& p : q) {   // non-negative shifts (up_only): [p, p + ypad]
+          pts.push_back({p[0], p[1] - (up_only ? 0.0 : ypad), p[2]});
           pts.push_back({p[0], p[1] + ypad, p[2]});
         }
       }
@@ -183,7 +184,8 @@ bool hulls_separated(const P3* A, int na, const P3* B, int nb, double margin, P3
   return hull_gap(A, na, B, nb, v) > margin;   // the exact check along v
 }
 
-bool leaf_hull_points(const FlatScene& fs, const dtd::DNodeDev& leaf, int skip_shape, double ypad, std::vector<P3>& out)
+bool leaf_hull_points(const FlatScene& fs, const dtd::DNodeDev& leaf, int skip_shape, double ypad, std::vector<P3>& out,
+                      bool up_only)
 {
   out.clear();
   const int nq = (leaf.meta & dtd::DN_SINGLE) ? 1 : (int)leaf.aux;
@@ -191,7 +193,7 @@ bool leaf_hull_points(const FlatScene& fs, const dtd::DNodeDev& leaf, int skip_s
     const int sid = (leaf.meta & dtd::DN_SINGLE) ? (int)leaf.first : fs.bvh.leaf_idx[leaf.first + q];
     if (sid == skip_shape) continue;
     if (sid < 0 || sid >= (int)fs.hdr.size() ||
-        !shape_hull_points(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, ypad, out)) {
+        !shape_hull_points(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, ypad, out, up_only)) {
       out.clear();
       return false;
     }

@@ -55,9 +55,11 @@ inline P3 sub3(const P3& a, const P3& b) { return {a[0] - b[0], a[1] - b[1], a[2
 inline P3 mad3(const P3& a, const P3& b, double s) { return {a[0] + s * b[0], a[1] + s * b[1], a[2] + s * b[2]}; }
 // points whose hull holds every hit a planar shape's float tests can report (moving named
 // rectangles: also shifted by +-ypad in y); false for spheres and cylinders
-bool shape_hull_points(const dtd::DShapeHdr& h, const double* g, double ypad, std::vector<P3>& pts);
+bool shape_hull_points(const dtd::DShapeHdr& h, const double* g, double ypad, std::vector<P3>& pts,
+                       bool up_only = false);
 // the hull points of a leaf's shapes but `skip_shape`; false (empty) when one has none
-bool leaf_hull_points(const FlatScene& fs, const dtd::DNodeDev& leaf, int skip_shape, double ypad, std::vector<P3>& out);
+bool leaf_hull_points(const FlatScene& fs, const dtd::DNodeDev& leaf, int skip_shape, double ypad, std::vector<P3>& out,
+                      bool up_only = false);
 // min over A minus max over B of the projections on v, in units of |v|
 double hull_gap(const P3* A, int na, const P3* B, int nb, const P3& v);
 // are the hulls of A and B more than `margin` apart? (GJK direction, then the exact gap along it;
@@ -108,6 +110,7 @@ struct Accel {
   std::vector<int32_t> leaf;           // leaf_idx (never empty)
   int n_fnodes = 0, n_bnodes = 0;
   float bump_pad = 0;
+  bool bump_up_only = false;           // every blur shift >= 0 (blur_leaf_pad)
   int ftree_mode = 0;
   int boxes_ordered = 0;
   ShadowGrid sg;

@@ -569,7 +569,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
             shull.clear();
             for (int sid : shp)
               if (sid != L.shape_index &&
-                  !shape_hull_points(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, ypad, shull)) {
+                  !shape_hull_points(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, ypad, shull, up_only)) {
                 shull.clear();
                 break;
               }
