@@ -69,13 +69,21 @@ def accel_info(built, g):
 
 
 class Scene:
-    """Device-resident scene + reference-topology BVH (dt_scene_create)."""
+    """Device-resident scene + reference-topology BVH (dt_scene_create). upload=False runs only the
+    host half (dt_scene_prepare: no device work, safe beside a running render); upload() or the
+    first render does the device half (dt_scene_upload)."""
 
-    def __init__(self, built, g):
+    def __init__(self, built, g, upload=True):
         self._h = ctypes.c_void_p()
         desc = built._ptr if isinstance(built, BuiltScene) else ctypes.pointer(built)
         self._keep = built
-        check(lib.dt_scene_create(desc, ctypes.byref(g), ctypes.byref(self._h)), "dt_scene_create")
+        if upload:
+            check(lib.dt_scene_create(desc, ctypes.byref(g), ctypes.byref(self._h)), "dt_scene_create")
+        else:
+            check(lib.dt_scene_prepare(desc, ctypes.byref(g), ctypes.byref(self._h)), "dt_scene_prepare")
+
+    def upload(self):
+        check(lib.dt_scene_upload(self._h), "dt_scene_upload")
 
     @property
     def handle(self):

@@ -70,13 +70,30 @@ int fail(int code, const std::string& msg)
       return fail(DT_E_NO_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));  \
   } while (0)
 
+// Scene uploads go through a non-blocking stream of the calling thread: a plain hipMemcpy runs on
+// the legacy null stream and waits for every kernel in flight, so a scene built on a worker
+// thread while the previous frame renders (tools/animate.py) would wait for that render.
+static hipStream_t upload_stream()
+{
+  thread_local hipStream_t s = nullptr;
+  if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+  return s;
+}
+
 template <class T>
 int upload(const std::vector<T>& v, void** dptr)
 {
   size_t bytes = v.size() * sizeof(T);
   if (bytes == 0) bytes = 16;
   HIPCHK(hipMalloc(dptr, bytes));
-  if (!v.empty()) HIPCHK(hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  if (v.empty()) return DT_OK;
+  hipStream_t us = upload_stream();
+  if (!us) {
+    HIPCHK(hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return DT_OK;
+  }
+  HIPCHK(hipMemcpyAsync(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, us));
+  HIPCHK(hipStreamSynchronize(us));
   return DT_OK;
 }
 
@@ -129,6 +146,10 @@ struct dt_scene {
   float* h_zs = nullptr;          // pinned staging for the cloud z sequence
   bool copy_pending = false;
   bool timed = false;
+  bool launched = false;   // a trace launch was enqueued (may still read device-side lists)
+  bool uploaded = false;   // dt_scene_upload ran (dt_scene_prepare builds on the host only)
+  bool pl_dirty = false;   // the host primary lists changed since their last upload
+  Accel acc;               // host acceleration structures until the upload
   // primary-ray candidate lists, rebuilt when the camera / resolution changes (host_primlists.cpp)
   std::vector<dtd::DNodeDev> fnodes_host, bnodes_host;
   std::vector<std::vector<P3>> fhull, bhull;   // leaf hull points per fast / bump tree node (host_hull.cpp)
@@ -200,7 +221,18 @@ void dt_globals_default(dt_globals* g)
   g->seed = 0;
 }
 
-int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** out)
+static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame, const dt_tiles* tiles,
+                          dtd::DParams& P, std::vector<float>& zs);
+static int update_primary_lists(dt_scene* sc, dtd::DParams& P, bool upload_now);
+static int upload_primary_lists(dt_scene* sc);
+
+static int scene_upload(dt_scene* s);
+
+// Host half of dt_scene_create: flatten, BVH, acceleration structures, hulls and the primary-ray
+// lists for the globals' camera. No device work, so it can run on a worker thread beside a render
+// that fills the GPU (the persistent trace kernel holds every CU, so even a copy's blit kernel
+// would wait for it: tools/animate.py builds frame n+1 this way and uploads it between frames).
+int dt_scene_prepare(const dt_scene_desc* desc, const dt_globals* g, dt_scene** out)
 {
   if (!desc || !g || !out) return fail(DT_E_INVALID, "null argument");
   *out = nullptr;
@@ -227,7 +259,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
     return fail(DT_E_NO_DEVICE, "no HIP device");
   }
   const FlatScene& f = s->flat;
-  Accel acc;
+  Accel& acc = s->acc;
   build_accel(f, *g, acc, stage);
   s->n_fnodes = acc.n_fnodes;
   s->n_bnodes = acc.n_bnodes;
@@ -246,27 +278,59 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
     for (int i = 0; i < s->n_bnodes; ++i)
       if (s->bnodes_host[i].meta & dtd::DN_LEAF) leaf_hull_points(f, s->bnodes_host[i], -1, (double)s->bump_pad, s->bhull[i], acc.bump_up_only);
   }
-  if ((rc = upload(s->sg.cells, &s->d_sg_cells)) || (rc = upload(s->sg.list, &s->d_sg_list))) {
-    dt_scene_destroy(s);
-    return rc;
+  {   // the primary-ray lists for the globals' camera and resolution; a render with another
+      // camera rebuilds them
+    dtd::DParams P;
+    std::vector<float> zs;
+    dt_tiles whole;
+    memset(&whole, 0, sizeof(whole));
+    whole.world = 1;
+    if (prepare_render(s, g, 0, &whole, P, zs) == DT_OK) (void)update_primary_lists(s, P, false);
+    stage("primary lists");
   }
-  if ((rc = upload(acc.dnodes, &s->d_nodes)) || (rc = upload(acc.fnodes, &s->d_fnodes)) ||
+  *out = s;
+  return DT_OK;
+}
+
+// Device half: allocations and uploads of everything dt_scene_prepare built (a few ms)
+static int scene_upload(dt_scene* s)
+{
+  if (s->uploaded) return DT_OK;
+  const FlatScene& f = s->flat;
+  const Accel& acc = s->acc;
+  int rc;
+  if ((rc = upload(s->sg.cells, &s->d_sg_cells)) || (rc = upload(s->sg.list, &s->d_sg_list)) ||
+      (rc = upload(acc.dnodes, &s->d_nodes)) || (rc = upload(acc.fnodes, &s->d_fnodes)) ||
       (rc = upload(acc.bnodes, &s->d_bnodes)) || (rc = upload(acc.bparent, &s->d_bparent)) || (rc = upload(acc.leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
       (rc = upload(f.geom, &s->d_geom)) || (rc = upload(f.mat, &s->d_mat)) || (rc = upload(f.lights, &s->d_lights)) ||
-      (rc = upload(f.tex, &s->d_tex))) {
-    dt_scene_destroy(s);
+      (rc = upload(f.tex, &s->d_tex)))
     return rc;
-  }
   if (hipMalloc((void**)&s->d_stats, sizeof(unsigned long long) * (ST_N + 1 + DT_N_STAMPS)) != hipSuccess ||
       hipMalloc(&s->d_launch, dt_launch_size()) != hipSuccess || hipEventCreate(&s->ev0) != hipSuccess ||
       hipEventCreate(&s->ev1) != hipSuccess || hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void**)&s->h_launch, dt_launch_size(), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc((void**)&s->h_zs, 2048 * sizeof(float), hipHostMallocDefault) != hipSuccess) {
-    dt_scene_destroy(s);
+      hipHostMalloc((void**)&s->h_zs, 2048 * sizeof(float), hipHostMallocDefault) != hipSuccess)
     return fail(DT_E_NO_DEVICE, "device allocation failed");
+  s->uploaded = true;
+  return DT_OK;
+}
+
+int dt_scene_upload(dt_scene* s)
+{
+  if (!s) return fail(DT_E_INVALID, "null scene");
+  if (int rc = scene_upload(s)) return rc;
+  return upload_primary_lists(s);   // the primary lists dt_scene_prepare built
+}
+
+int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** out)
+{
+  int rc = dt_scene_prepare(desc, g, out);
+  if (rc) return rc;
+  if ((rc = dt_scene_upload(*out))) {
+    dt_scene_destroy(*out);
+    *out = nullptr;
+    return rc;
   }
-  stage("upload");
-  *out = s;
   return DT_OK;
 }
 
@@ -423,7 +487,7 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
 // Primary-ray candidate lists for P's camera (DT_PRIM_LISTS=0 disables them; DT_PL_BLOCK: pixels
 // per block side, default 8). Rebuilt only when the camera or resolution changes; the device copy
 // is replaced after the device has drained, since earlier launches may still read it.
-static int update_primary_lists(dt_scene* sc, dtd::DParams& P)
+static int update_primary_lists(dt_scene* sc, dtd::DParams& P, bool upload_now)
 {
   P.pl_block = P.pl_nbx = P.pl_nby = P.pl_bump = 0;
   const char* e = getenv("DT_PRIM_LISTS");
@@ -443,8 +507,8 @@ static int update_primary_lists(dt_scene* sc, dtd::DParams& P)
                              (double)hull, (double)SB, (double)bump};
   for (int k = 0; k < 3; ++k) key.insert(key.end(), {P.eye[k], P.X[k], P.Y[k], P.Z[k]});
   if (key != sc->pl_key) {
-    HIPCHK(hipDeviceSynchronize());
     sc->pl_key = key;
+    sc->pl_dirty = true;
     sc->pl_ok = build_primary_lists(sc->fnodes_host, sc->n_fnodes, P, B, sc->pl, hull ? &sc->fhull : nullptr, SB);
     sc->pl_bump = false;
     PrimLists pb_lists;
@@ -459,18 +523,9 @@ static int update_primary_lists(dt_scene* sc, dtd::DParams& P)
       sc->pl.list.insert(sc->pl.list.end(), pb_lists.list.begin(), pb_lists.list.end());
       sc->pl_bump = true;
     }
-    if (sc->d_pl_cells) (void)hipFree(sc->d_pl_cells);
-    if (sc->d_pl_list) (void)hipFree(sc->d_pl_list);
-    sc->d_pl_cells = sc->d_pl_list = nullptr;
-    if (sc->pl_ok) {
-      int rc;
-      if ((rc = upload(sc->pl.cells, &sc->d_pl_cells)) || (rc = upload(sc->pl.list, &sc->d_pl_list))) {
-        sc->pl_ok = false;
-        sc->pl_key.clear();
-        return rc;
-      }
-    }
   }
+  if (upload_now)
+    if (int rc = upload_primary_lists(sc)) return rc;
   if (sc->pl_ok) {
     P.pl_block = sc->pl.block;
     P.pl_nbx = sc->pl.nbx;
@@ -480,10 +535,32 @@ static int update_primary_lists(dt_scene* sc, dtd::DParams& P)
   return DT_OK;
 }
 
+// device copy of the host primary lists, replaced after the device has drained (earlier launches
+// may still read the old one)
+static int upload_primary_lists(dt_scene* sc)
+{
+  if (!sc->pl_dirty || !sc->uploaded) return DT_OK;
+  if (sc->launched) HIPCHK(hipDeviceSynchronize());
+  if (sc->d_pl_cells) (void)hipFree(sc->d_pl_cells);
+  if (sc->d_pl_list) (void)hipFree(sc->d_pl_list);
+  sc->d_pl_cells = sc->d_pl_list = nullptr;
+  sc->pl_dirty = false;
+  if (sc->pl_ok) {
+    int rc;
+    if ((rc = upload(sc->pl.cells, &sc->d_pl_cells)) || (rc = upload(sc->pl.list, &sc->d_pl_list))) {
+      sc->pl_ok = false;
+      sc->pl_key.clear();
+      return rc;
+    }
+  }
+  return DT_OK;
+}
+
 static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>& zs, float* out_dev,
                           hipStream_t st)
 {
-  if (int rc = update_primary_lists(sc, P)) return rc;
+  if (int rc = scene_upload(sc)) return rc;
+  if (int rc = update_primary_lists(sc, P, true)) return rc;
   // Fully asynchronous: the launch record and z table go through pinned staging that is
   // only rewritten after the previous call's copies have executed (ev_copy); the device
   // copies themselves are stream-ordered after any earlier kernel that reads them.
@@ -559,6 +636,7 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   if (PL.sky_defer) HIPCHK(dt_launch_sky_miss(sc->d_launch, out_dev, n_px, st));
   HIPCHK(hipEventRecord(sc->ev1, st));
   sc->timed = true;
+  sc->launched = true;
   sc->last = P;
   return DT_OK;
 }
@@ -567,6 +645,7 @@ int dt_collect_stats(const dt_scene* sc_c, void* stream, dt_stats* stats)
 {
   dt_scene* sc = const_cast<dt_scene*>(sc_c);
   if (!sc) return fail(DT_E_INVALID, "null scene");
+  if (!sc->uploaded) return fail(DT_E_INVALID, "scene not uploaded (dt_scene_upload)");
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipStreamSynchronize(st));
   if (!stats) return DT_OK;
@@ -818,6 +897,7 @@ int dt_write_png(const char* filename, int32_t xRes, int32_t yRes, const float* 
 extern "C" int dt_debug_counters(const dt_scene* sc, uint64_t* out, int32_t n)
 {
   if (!sc || !out || n < 0 || n > DT_N_STAMPS) return fail(DT_E_INVALID, "bad arguments");
+  if (!sc->uploaded) return fail(DT_E_INVALID, "scene not uploaded (dt_scene_upload)");
   std::vector<unsigned long long> h(ST_N + 1 + DT_N_STAMPS);
   HIPCHK(hipMemcpy(h.data(), sc->d_stats, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
   for (int i = 0; i < n; ++i) out[i] = h[ST_N + 1 + i];

@@ -194,8 +194,9 @@ enum dt_out_layout {
 typedef struct dt_tiles {
   int32_t x0, y0, x1, y1;    /* pixel window [x0,x1) x [y0,y1); x1<=0 means full width/height */
   int32_t tile_w, tile_h;    /* tile size (<=0: 32x32) */
-  int32_t rank, world;       /* tile t (row-major over the window's tile grid) is owned by
-                                rank t % world */
+  int32_t rank, world;       /* the window's tiles (row-major) fall into groups of `world`
+                                consecutive tiles; each rank owns one tile of every group, the
+                                ranks rotated by a hash of the group (dt_scene_dev.h tile_of) */
   int32_t layout;            /* dt_out_layout */
   int32_t _pad;
 } dt_tiles;
@@ -235,6 +236,13 @@ void dt_globals_default(dt_globals* g);
  * scene to the current HIP device. */
 int  dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** out);
 void dt_scene_destroy(dt_scene* s);
+/* dt_scene_create in two halves. dt_scene_prepare does the host work (flatten, BVH, acceleration
+ * structures, primary-ray lists) and touches no device memory, so it can run on a worker thread
+ * while a render fills the GPU; dt_scene_upload allocates and uploads (a few ms). A render of a
+ * scene that was prepared but not uploaded uploads it first. No reference counterpart: the
+ * reference builds its BVH inside renderImage (render_final_project.cpp:965-1030). */
+int  dt_scene_prepare(const dt_scene_desc* desc, const dt_globals* g, dt_scene** out);
+int  dt_scene_upload(dt_scene* s);
 
 /* BVH export for parity tests: node i = {first child or -1, n_children, first shape,
  * n_shapes, leaf, lbound[3], ubound[3]} in the reference's push order. */
