@@ -306,6 +306,26 @@ def test_shadow_grid_pass0_lists(cuda, monkeypatch, frame):
         assert np.array_equal(img, ref_img), mode
 
 
+def test_scene_prepare_then_upload(cuda):
+    """dt_scene_prepare (host only) + dt_scene_upload, or a render of a prepared scene (which
+    uploads it first), give dt_scene_create's image: C2 window."""
+    g = dt.globals_default()
+    g.use_model = 0
+    built = dt.build_scene("final", 240, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.brdf_samples = 800, 600, 16, 4, 2
+    tile = dt.tiles(x0=380, y0=250, x1=420, y1=280)
+    ref, ref_st = _render_gpu(built, g, 240, tile)
+    for explicit in (True, False):
+        scene = dt.Scene(built, g, upload=False)
+        if explicit:
+            scene.upload()
+        out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
+        st = dt.render(scene, g, 240, out, tile)
+        scene.close()
+        assert st.rays == ref_st.rays
+        assert np.array_equal(out.cpu().numpy(), ref), explicit
+
+
 PL_CASES = [  # (name, builder, frame, models, W, H, spp, depth, window)
     ("c3", "final", 240, 0, 1920, 1080, 64, 8, (880, 480, 1008, 560)),
     ("c4-models", "final", 240, 1, 1920, 1080, 16, 3, (1200, 500, 1296, 580)),
