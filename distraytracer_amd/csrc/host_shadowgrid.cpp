@@ -158,10 +158,17 @@ bool shape_separated(const dtd::DShapeHdr& h, const double* g, const double clo[
                      const double llo[3], const double lhi[3], double margin, double ypad)
 {
   double mn, mx;
-  const double m = margin + ((h.flags & DT_F_NAMED_RECT) ? ypad : 0.0);
+  double m = margin + ((h.flags & DT_F_NAMED_RECT) ? ypad : 0.0);
   switch (h.type) {
     case DT_SHAPE_RECTANGLE: {
       const double* R = g + dtd::RC_R;
+      if (h.flags & DT_F_NAMED_RECT) {
+        // a shift by s in y moves the plane by s * |n_y| / |n| along its normal (tunnel panels
+        // with near-horizontal normals barely move), so that is all the margin it needs
+        const double* n = R + dtd::R_N;
+        const double nn = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        if (nn > 0) m = margin + ypad * std::fabs(n[1]) / nn * (1 + 1e-9) + 1e-9 * ypad;
+      }
       return plane_range(R + dtd::R_A, R + dtd::R_N, clo, chi, llo, lhi, mn, mx) && (mn > m || mx < -m);
     }
     case DT_SHAPE_CHECKERBOARD:
