@@ -59,8 +59,8 @@ def cpu_baseline(dt, cfg, frac_world):
     dt1 = time.perf_counter() - t1
     return {"value": round(st.samples / dt_s / 1e6, 4), "unit": "Mpixel-samples/s", "cores": threads,
             "kind": "port",
-            "sample": "oracle/oracle.c (OpenMP) on 1/%d of the frame's 32x32 tiles (rank-0 of a %d-way "
-                      "interleave: %d pixels x %d spp), %.1f s wall" % (frac_world, frac_world, st.pixels,
+            "sample": "oracle/oracle.c (OpenMP) on 1/%d of the frame's 32x32 tiles (rank 0's share of a %d-way "
+                      "tile split: %d pixels x %d spp), %.1f s wall" % (frac_world, frac_world, st.pixels,
                                                                     st.samples // max(st.pixels, 1), dt_s),
             "single_core": {"value": round(st1.samples / dt1 / 1e6, 4), "cores": 1,
                             "sample": "1/%d of the tiles, %.1f s" % (frac_world * 16, dt1)}}
