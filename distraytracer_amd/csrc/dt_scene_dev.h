@@ -98,7 +98,8 @@ enum { CK_R = 0, CK_GN = 14, CK_A = 17, CK_B = 20, CK_C = 23, CK_D = 26, CK_HOLE
        CK_MVD = 61, CK_BW = 62, CK_SIZE = 63 };
 
 #define DT_MAX_SGRID 16        // lights with a shadow grid (host_shadowgrid.cpp)
-#define DT_SGRID_MAX_LIST 48   // longer candidate lists: the cell walks the tree instead
+#define DT_SGRID_MAX_LIST 96   // longer candidate lists: the cell walks the tree instead
+#define DT_SG_REACH_DEFAULT 0.25f   // a cell's list covers points this many cells outside it
 #define DT_SG_WALK 0xffffffffu   // cell record count: the list was too long, walk the tree
 #define DT_SG_UMBRA 0x80000000u  // cell record offset flag: every segment to the light is occluded (host_shadowgrid.cpp)
 

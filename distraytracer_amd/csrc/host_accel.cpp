@@ -102,12 +102,14 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
   if (a.bnodes.empty()) a.bnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
   if (a.bparent.empty()) a.bparent.push_back(-1);
   stage("bump tree");
-  // shadow grid (host_shadowgrid.cpp); DT_SHADOW_GRID=0: every shadow test walks a tree
+  // shadow grid (host_shadowgrid.cpp); DT_SHADOW_GRID=0: every shadow test walks a tree.
+  // Reach 0.25 cells and lists of up to 96 leaves (round 1: 0.5, 48): C3 +0.6%, C2 +0.5%, C4 +0.2%,
+  // C5 transition frame 1088 -9%, tunnel frames -2% (profiles/r02bj_ab_reach_cap.log)
   const char* sgv = getenv("DT_SHADOW_GRID");
   const char* sgc = getenv("DT_SG_CELLS");
   const char* sgr = getenv("DT_SG_REACH");
   if ((sgv && sgv[0] == '0') ||
-      !build_shadow_grid(dnodes, f, a.sg, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : 0.5f,
+      !build_shadow_grid(dnodes, f, a.sg, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : DT_SG_REACH_DEFAULT,
                          a.n_bnodes > 0 ? (double)a.bump_pad : 0.0, up_only))
     a.sg = ShadowGrid();
   for (int l = 0; l < DT_MAX_SGRID; ++l) a.sg.base0[l] = a.sg.base[l];
@@ -121,7 +123,7 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
     const char* p0 = getenv("DT_SG_PASS0");
     const bool want = p0 ? p0[0] == '1' : walk > cells / 10;
     ShadowGrid g0;
-    if (want && build_shadow_grid(dnodes, f, g0, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : 0.5f, 0.0) &&
+    if (want && build_shadow_grid(dnodes, f, g0, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : DT_SG_REACH_DEFAULT, 0.0) &&
         g0.n_lights == a.sg.n_lights && g0.dim[0] == a.sg.dim[0] && g0.dim[1] == a.sg.dim[1] && g0.dim[2] == a.sg.dim[2]) {
       const uint32_t cell_off = (uint32_t)(a.sg.cells.size() / 2), list_off = (uint32_t)a.sg.list.size();
       for (size_t c = 0; c < g0.cells.size(); c += 2) {

@@ -193,11 +193,12 @@ def _accel(name, frame, models, env, monkeypatch):
 
 
 def test_shadow_grid_pass0_grid_appended(monkeypatch):
-    """Frame 1920's blur shifts (<= 81) pad the lists until many cells walk (over the 10% that
-    appends a pass-0 grid by default); the pass-0 grid (same cells, unpadded lists) walks almost
-    nowhere."""
-    pad = _accel("c5-1920", 1920, 0, {}, monkeypatch)
-    both = _accel("c5-1920", 1920, 0, {"DT_SG_PASS0": "1"}, monkeypatch)
+    """Frame 1920's blur shifts (<= 81) pad the lists; with a short list cap (24) many cells walk
+    (over the 10% that appends a pass-0 grid by default), and the pass-0 grid (same cells, unpadded
+    lists) walks almost nowhere. With the default cap (96) no cell walks and nothing is appended."""
+    cap = {"DT_SG_MAX_LIST": "24"}
+    pad = _accel("c5-1920", 1920, 0, cap, monkeypatch)
+    both = _accel("c5-1920", 1920, 0, dict(cap, DT_SG_PASS0="1"), monkeypatch)
     assert pad["sg_tree_cells"] > pad["sg_cells"] // 10
     assert both["sg_cells"] == 2 * pad["sg_cells"]
     assert both["sg_tree_cells"] - pad["sg_tree_cells"] < pad["sg_cells"] // 20
@@ -206,6 +207,11 @@ def test_shadow_grid_pass0_grid_appended(monkeypatch):
     g.use_model = 0
     dflt = dt.accel_info(dt.build_scene("final", 1920, g), g)
     assert dflt["sg_cells"] == both["sg_cells"]
+    monkeypatch.delenv("DT_SG_MAX_LIST")
+    g = dt.globals_default()
+    g.use_model = 0
+    dflt96 = dt.accel_info(dt.build_scene("final", 1920, g), g)
+    assert dflt96["sg_cells"] == pad["sg_cells"] and dflt96["sg_tree_cells"] <= pad["sg_cells"] // 10
 
 
 # C3's room, C4's meshes (2442 leaves), a C5 tunnel frame with blur-padded lists
