@@ -15,3 +15,4 @@ if [ -z "$NO_C5" ]; then timeout -k 10 300 python tools/animate.py --frames 0:30
 cd /tmp; export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 $R/bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > $O/kt.log 2>&1
 echo all done
+if [ -n "$TORCHRUN" ]; then timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 $R/bench.py --gpus 1 --steps 5 --warmup 1 --no-cpu-baseline > $O/torchrun_n1.json 2> $O/torchrun_n1.err; echo torchrun ok; fi
