@@ -76,7 +76,12 @@ int fail(int code, const std::string& msg)
 static hipStream_t upload_stream()
 {
   thread_local hipStream_t s = nullptr;
+  thread_local int s_dev = -1;   // streams belong to a device: a thread that switches gets a new one
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (s && s_dev != dev) s = nullptr;   // the old device's stream stays valid for its device
   if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+  s_dev = dev;
   return s;
 }
 
