@@ -2312,16 +2312,15 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       pixel_of(P, item * group + lane, qx, qy, qo, qv);
       if (qv && !(P.sky_defer && S.sky_miss[item * group + lane])) {
         V3 color = divs(v3(psum[0][lane], psum[1][lane], psum[2][lane]), spp);
-#ifdef DT_ITEM_TIMES   // diagnostic builds: the item's wave cycles / 1e4 in every channel
-        color = v3(1, 1, 1);
+#ifdef DT_ITEM_TIMES   // diagnostic builds (tools/item_times.py): the item's wave cycles / 1e4, raw
         {
           const float cyc = (float)(__builtin_amdgcn_s_memtime() - item_t0) * 1e-4f;
           const int64_t off = P.layout == DT_OUT_SLAB ? qo : 3 * ((int64_t)(P.yRes - 1 - qy) * P.xRes + qx);
           out[off] = cyc; out[off + 1] = cyc; out[off + 2] = cyc;
         }
-        if (false)
-#endif
+#else
         store_pixel(P, out, qx, qy, qo, color);
+#endif
         if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
       }
     }
@@ -2374,26 +2373,10 @@ dt_sky_miss_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     pt.x = ((P.sky_m[0][0] * fp.x + P.sky_m[0][1] * fp.y) + P.sky_m[0][2] * fp.z) + P.sky_m[0][3] * 1.0;
     pt.y = ((P.sky_m[1][0] * fp.x + P.sky_m[1][1] * fp.y) + P.sky_m[1][2] * fp.z) + P.sky_m[1][3] * 1.0;
     pt.z = ((P.sky_m[2][0] * fp.x + P.sky_m[2][1] * fp.y) + P.sky_m[2][2] * fp.z) + P.sky_m[2][3] * 1.0;
-#ifdef DT_SKYMISS_DEBUG   // diagnostic builds: the march input point, raw
-    if (valid) {
-      const int64_t off = P.layout == DT_OUT_SLAB ? so : 3 * ((int64_t)(P.yRes - 1 - y) * P.xRes + x);
-      const V3 sk = sky_color(P, pt);
-      int nd = 0;
-      float dsum = 0;
-      for (int k = 0; k < P.n_cloud_steps; ++k) {
-        const float d = cloud_step(P, S.cloud_z[k], pt);
-        if (d >= 0.0f) { ++nd; dsum += d; }
-      }
-      out[off] = (float)sk.x; out[off + 1] = (float)nd; out[off + 2] = dsum;
-    }
-    if (false)
-#endif
-    {
     const V3 color = cloud_color_lane(P, S.cloud_z, pt);
     if (valid) {
       store_pixel(P, out, x, y, so, color);
       if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
-    }
     }
   }
   const unsigned long long n = __popcll(__ballot(mine));

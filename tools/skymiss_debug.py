@@ -1,5 +1,7 @@
-"""Diagnostic: the deferred sky march's input points (-DDT_SKYMISS_DEBUG build via DT_LIB) against
-the host's mcam * focalPoint, and the default build's colours with and without DT_SKY_DEFER."""
+"""Diagnostic: colours of a few C5 cloud-frame pixels through the deferred per-lane sky and (with
+DT_SKY_DEFER=0) the cooperative march; SKY2000=1 also compares renderImageCloud at frame 2000 with
+the oracle. Written while finding why a called (not inlined) cloud_color_lane returned wrong colours
+(DESIGN.md §4)."""
 import os
 import sys
 
