@@ -485,6 +485,8 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   P.sg_ypad = (float)sc->sg.ypad;
 
   P.n_lights = (int32_t)sc->flat.lights.size();
+  P.ls_first = 0;
+  while (P.ls_first < P.n_lights && sc->flat.lights[P.ls_first].type != DT_LIGHT_RECT) ++P.ls_first;
   P.n_shapes = (int32_t)sc->flat.hdr.size();
   return DT_OK;
 }

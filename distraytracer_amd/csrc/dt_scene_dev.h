@@ -131,6 +131,7 @@ struct DParams {
   int32_t n_cloud_steps;
   int32_t item_batch;     // wave items per queue atomic (dt_api.cpp: 2 when waves take >= 64 items, else 1)
   int32_t prio_steps;     // DFS steps after which a wave raises its issue priority (0: never)
+  int32_t ls_first;       // first area (rectangle) light: where the light-sample cache starts
   int32_t sky_defer;      // 1 spp: missed pixels are flagged, dt_sky_miss_kernel marches them per lane
   uint32_t seed;
   float aperture, focal_length, near_plane;
