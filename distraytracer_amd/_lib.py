@@ -21,7 +21,8 @@ DT_OUT_IMAGE = 0
 DT_OUT_SLAB = 1
 
 SHAPE_TYPES = {1: "sphere", 2: "cylinder", 3: "triangle", 4: "rectangle", 5: "rectprism_v2",
-               6: "checkerboard", 7: "checkerboard_hole", 8: "checker_cylinder"}
+               6: "checkerboard", 7: "checkerboard_hole", 8: "checker_cylinder", 9: "rectprism_cyl"}
+ABI_VERSION = 2
 
 
 class ShapeDesc(ctypes.Structure):
@@ -30,7 +31,7 @@ class ShapeDesc(ctypes.Structure):
                 ("S", c_float), ("borderwidth", c_float), ("length", c_float), ("width", c_float),
                 ("refr", c_double * 2), ("color", D3), ("color1", D3), ("color2", D3),
                 ("bordercolor", D3), ("center", D3), ("v", D3 * 8), ("mesh_normal", D3),
-                ("uv", (c_double * 2) * 3)]
+                ("uv", (c_double * 2) * 3), ("hole_first", c_int32), ("n_holes", c_int32)]
 
 
 class LightDesc(ctypes.Structure):
@@ -46,7 +47,8 @@ class TextureDesc(ctypes.Structure):
 class SceneDesc(ctypes.Structure):
     _fields_ = [("n_shapes", c_int32), ("n_lights", c_int32), ("n_textures", c_int32), ("_pad", c_int32),
                 ("shapes", ctypes.POINTER(ShapeDesc)), ("lights", ctypes.POINTER(LightDesc)),
-                ("textures", ctypes.POINTER(TextureDesc))]
+                ("textures", ctypes.POINTER(TextureDesc)), ("n_holes", c_int32), ("_pad2", c_int32),
+                ("holes", ctypes.POINTER(ShapeDesc))]
 
 
 class Globals(ctypes.Structure):
@@ -140,6 +142,10 @@ def _load():
         raise DTError("libdt.so not built (%s): run __graft_entry__.build() / make -C "
                       "distraytracer_amd/csrc" % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
+    lib.dt_abi_version.restype = c_int32
+    if lib.dt_abi_version() != ABI_VERSION:   # a stale library would misread every descriptor
+        raise DTError("libdt.so ABI %d, this binding expects %d: rebuild (make -C distraytracer_amd/csrc)"
+                      % (lib.dt_abi_version(), ABI_VERSION))
     P = ctypes.POINTER
     sig = {
         "dt_abi_version": (c_int32, []),

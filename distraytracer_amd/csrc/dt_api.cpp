@@ -25,6 +25,8 @@ extern "C" hipError_t dt_launch_sky_miss(const void* dev_launch, float* out, int
 extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_t slab_floats, const float* slabs,
                                        float* image, hipStream_t stream);
 extern "C" const void* dt_trace_kernel_ptr(void);
+extern "C" hipError_t dt_launch_trace_rpc(const void* dev_launch, float* out, int grid, hipStream_t stream);
+extern "C" const void* dt_trace_kernel_rpc_ptr(void);
 
 namespace {
 
@@ -130,6 +132,8 @@ struct dt_scene {
   void* d_bparent = nullptr;
   int n_bnodes = 0;
   float bump_pad = 0;          // y padding of its leaves: the largest |shift| a blur pass can draw
+  bool bump_up_only = false;   // bump tree / blur-padded lists built for shifts >= 0 only
+  bool no_cull = false;        // a RectPrismWithCylinder: no t-culling, no grid, no primary lists
   ShadowGrid sg;
   void* d_sg_cells = nullptr;
   void* d_sg_list = nullptr;
@@ -269,6 +273,8 @@ int dt_scene_prepare(const dt_scene_desc* desc, const dt_globals* g, dt_scene** 
   s->n_fnodes = acc.n_fnodes;
   s->n_bnodes = acc.n_bnodes;
   s->bump_pad = acc.bump_pad;
+  s->bump_up_only = acc.bump_up_only;
+  s->no_cull = acc.no_cull;
   s->ftree_mode = acc.ftree_mode;
   s->boxes_ordered = acc.boxes_ordered;
   s->sg = std::move(acc.sg);
@@ -297,7 +303,33 @@ int dt_scene_prepare(const dt_scene_desc* desc, const dt_globals* g, dt_scene** 
   return DT_OK;
 }
 
-// Device half: allocations and uploads of everything dt_scene_prepare built (a few ms)
+// every device buffer, event and pinned staging buffer of a scene, released and reset to null
+// (dt_scene_destroy, and a failed upload so that a retry starts from nothing)
+static void release_device(dt_scene* s)
+{
+  void** bufs[] = {&s->d_pl_cells, &s->d_pl_list, &s->d_nodes, &s->d_fnodes, &s->d_bnodes, &s->d_bparent,
+                   &s->d_sg_cells, &s->d_sg_list, &s->d_leaf, &s->d_hdr, &s->d_geom, &s->d_mat, &s->d_lights,
+                   &s->d_tex, &s->d_zs, (void**)&s->d_stats, &s->d_launch, (void**)&s->d_sky_miss};
+  for (void** b : bufs) {
+    if (*b) (void)hipFree(*b);
+    *b = nullptr;
+  }
+  for (hipEvent_t* e : {&s->ev0, &s->ev1, &s->ev_copy}) {
+    if (*e) (void)hipEventDestroy(*e);
+    *e = nullptr;
+  }
+  if (s->h_launch) (void)hipHostFree(s->h_launch);
+  if (s->h_zs) (void)hipHostFree(s->h_zs);
+  s->h_launch = nullptr;
+  s->h_zs = nullptr;
+  s->zs_cap = 0;
+  s->sky_miss_cap = 0;
+  s->copy_pending = s->timed = s->launched = false;
+  s->pl_dirty = true;   // the primary lists go up again with the next upload
+}
+
+// Device half: allocations and uploads of everything dt_scene_prepare built (a few ms). On a
+// failure everything allocated so far is released, so the next render's lazy upload retries cleanly.
 static int scene_upload(dt_scene* s)
 {
   if (s->uploaded) return DT_OK;
@@ -308,14 +340,18 @@ static int scene_upload(dt_scene* s)
       (rc = upload(acc.dnodes, &s->d_nodes)) || (rc = upload(acc.fnodes, &s->d_fnodes)) ||
       (rc = upload(acc.bnodes, &s->d_bnodes)) || (rc = upload(acc.bparent, &s->d_bparent)) || (rc = upload(acc.leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
       (rc = upload(f.geom, &s->d_geom)) || (rc = upload(f.mat, &s->d_mat)) || (rc = upload(f.lights, &s->d_lights)) ||
-      (rc = upload(f.tex, &s->d_tex)))
+      (rc = upload(f.tex, &s->d_tex))) {
+    release_device(s);
     return rc;
+  }
   if (hipMalloc((void**)&s->d_stats, sizeof(unsigned long long) * (ST_N + 1 + DT_N_STAMPS)) != hipSuccess ||
       hipMalloc(&s->d_launch, dt_launch_size()) != hipSuccess || hipEventCreate(&s->ev0) != hipSuccess ||
       hipEventCreate(&s->ev1) != hipSuccess || hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void**)&s->h_launch, dt_launch_size(), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc((void**)&s->h_zs, 2048 * sizeof(float), hipHostMallocDefault) != hipSuccess)
+      hipHostMalloc((void**)&s->h_zs, 2048 * sizeof(float), hipHostMallocDefault) != hipSuccess) {
+    release_device(s);
     return fail(DT_E_NO_DEVICE, "device allocation failed");
+  }
   s->uploaded = true;
   return DT_OK;
 }
@@ -342,15 +378,7 @@ int dt_scene_create(const dt_scene_desc* desc, const dt_globals* g, dt_scene** o
 void dt_scene_destroy(dt_scene* s)
 {
   if (!s) return;
-  void* bufs[] = {s->d_pl_cells, s->d_pl_list, s->d_nodes, s->d_fnodes, s->d_bnodes, s->d_bparent, s->d_sg_cells, s->d_sg_list, s->d_leaf, s->d_hdr, s->d_geom, s->d_mat, s->d_lights, s->d_tex, s->d_zs,
-                  s->d_stats, s->d_launch, s->d_sky_miss};
-  for (void* b : bufs)
-    if (b) (void)hipFree(b);
-  if (s->ev0) (void)hipEventDestroy(s->ev0);
-  if (s->ev1) (void)hipEventDestroy(s->ev1);
-  if (s->ev_copy) (void)hipEventDestroy(s->ev_copy);
-  if (s->h_launch) (void)hipHostFree(s->h_launch);
-  if (s->h_zs) (void)hipHostFree(s->h_zs);
+  release_device(s);
   delete s;
 }
 
@@ -469,6 +497,8 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   P.n_fnodes = sc->n_fnodes;
   P.n_bnodes = sc->n_bnodes;
   P.bump_pad = sc->bump_pad;
+  P.bump_up_only = sc->bump_up_only ? 1 : 0;
+  P.no_cull = sc->no_cull ? 1 : 0;
   P.ftree_mode = sc->ftree_mode;
   P.boxes_ordered = sc->boxes_ordered;
   P.sg_n = sc->sg.n_lights;
@@ -498,7 +528,7 @@ static int update_primary_lists(dt_scene* sc, dtd::DParams& P, bool upload_now)
 {
   P.pl_block = P.pl_nbx = P.pl_nby = P.pl_bump = 0;
   const char* e = getenv("DT_PRIM_LISTS");
-  if ((e && e[0] == '0') || sc->n_fnodes <= 0 || !(sc->ftree_mode & 1)) return DT_OK;
+  if ((e && e[0] == '0') || sc->n_fnodes <= 0 || !(sc->ftree_mode & 1) || sc->no_cull) return DT_OK;
   const char* b = getenv("DT_PL_BLOCK");
   const int B = b && atoi(b) > 0 ? atoi(b) : 8;
   // DT_PL_HULL=0: no hull culling; DT_PL_SUPER: blocks per super-block side (8); DT_PL_BUMP=0: the
@@ -542,12 +572,14 @@ static int update_primary_lists(dt_scene* sc, dtd::DParams& P, bool upload_now)
   return DT_OK;
 }
 
-// device copy of the host primary lists, replaced after the device has drained (earlier launches
-// may still read the old one)
+// device copy of the host primary lists, replaced once this scene's last trace launch has finished
+// (it may still read the old one). Launches of one scene are stream-ordered (they share its launch
+// record), so that is the event recorded after the last one; no device-wide barrier, which would
+// also wait for unrelated work such as an RCCL gather in flight.
 static int upload_primary_lists(dt_scene* sc)
 {
   if (!sc->pl_dirty || !sc->uploaded) return DT_OK;
-  if (sc->launched) HIPCHK(hipDeviceSynchronize());
+  if (sc->launched) HIPCHK(hipEventSynchronize(sc->ev1));
   if (sc->d_pl_cells) (void)hipFree(sc->d_pl_cells);
   if (sc->d_pl_list) (void)hipFree(sc->d_pl_list);
   sc->d_pl_cells = sc->d_pl_list = nullptr;
@@ -599,9 +631,13 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   hs.queue = sc->d_stats + ST_N;
   hs.pl_cells = (const uint32_t*)sc->d_pl_cells;
   hs.pl_list = (const uint32_t*)sc->d_pl_list;
-  static int resident = 0;
+  // scenes with a RectPrismWithCylinder take the trace kernel compiled with its tests (dt_kernels.hip
+  // DT_WITH_RPC), whose occupancy may differ
+  static int resident = 0, resident_rpc = 0;
   if (!resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
-  int64_t grid = P.n_items < resident ? P.n_items : resident;
+  if (sc->no_cull && !resident_rpc) resident_rpc = max_resident_waves(dt_trace_kernel_rpc_ptr(), 64);
+  const int64_t waves = sc->no_cull ? resident_rpc : resident;
+  int64_t grid = P.n_items < waves ? P.n_items : waves;
   if (grid < 1) grid = 1;
   // two items per queue atomic pays when every wave takes many items (C3: ~500, +2%); with few
   // (C2: ~30) the coarser tail costs more (-11%)
@@ -639,7 +675,8 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   sc->copy_pending = true;
   HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 1 + DT_N_STAMPS), st));
   HIPCHK(hipEventRecord(sc->ev0, st));
-  HIPCHK(dt_launch_trace(sc->d_launch, out_dev, (int)grid, st));
+  HIPCHK(sc->no_cull ? dt_launch_trace_rpc(sc->d_launch, out_dev, (int)grid, st)
+                     : dt_launch_trace(sc->d_launch, out_dev, (int)grid, st));
   if (PL.sky_defer) HIPCHK(dt_launch_sky_miss(sc->d_launch, out_dev, n_px, st));
   HIPCHK(hipEventRecord(sc->ev1, st));
   sc->timed = true;
@@ -729,7 +766,11 @@ int dt_render(const dt_scene* sc_c, const dt_globals* g, int32_t frame, const dt
                                          : (size_t)g->xRes * g->yRes * 3;
   if (!out_on_device) {
     HIPCHK(hipMalloc((void**)&dout, n_out * sizeof(float)));
-    HIPCHK(hipMemcpyAsync(dout, out, n_out * sizeof(float), hipMemcpyHostToDevice, st));
+    // a render that writes every float of the output (the whole image, one rank) needs no copy of
+    // the caller's buffer; otherwise the pixels it does not own keep the caller's values
+    const bool covers = P.layout == DT_OUT_IMAGE && P.world == 1 && P.x0 == 0 && P.y0 == 0 && P.x1 == g->xRes &&
+                        P.y1 == g->yRes;
+    if (!covers) HIPCHK(hipMemcpyAsync(dout, out, n_out * sizeof(float), hipMemcpyHostToDevice, st));
   }
   rc = enqueue_render(sc, P, zs, dout, st);
   if (rc == DT_OK && !out_on_device) {

@@ -51,6 +51,19 @@ using namespace dtd;
 #define DT_WORK(...)
 #endif
 
+// DT_WITH_RPC=1 (the second compilation of this file, build/dt_kernels_rpc.o): the trace kernel
+// dt_trace_kernel_rpc for scenes holding a RectPrismWithCylinder, with that shape's tests and no
+// t-culling (DParams::no_cull). Its code stays out of the hot dt_trace_kernel, whose register
+// allocation it would disturb (VGPR spills 196 -> 258 when compiled in).
+#ifndef DT_WITH_RPC
+#define DT_WITH_RPC 0
+#endif
+#if DT_WITH_RPC
+#define DT_TRACE_KERNEL dt_trace_kernel_rpc
+#else
+#define DT_TRACE_KERNEL dt_trace_kernel
+#endif
+
 #define DT_STACK_MAX 48
 #define DT_MAX_CLOUD_STEPS 2048
 #define DT_CLOUD_CHUNK 256
@@ -575,6 +588,145 @@ __device__ bool cyl_shadow(GP g, V3 ray, V3 start, float t_max)
   return cyl_in_caps(g, add(start, mul(t2, ray))) && t2 < t_max;
 }
 
+#if DT_WITH_RPC
+// Cylinder::intersectCap (geometry.cpp:297-324): the two cap PLANES (no radius test), c1.axis and
+// c2.axis precomputed (RH_C1A / RH_C2A)
+__device__ __forceinline__ bool cyl_cap(GP h, V3 ray, V3 start, float& t, int& inside)
+{
+  const float eps = 1e-3f;
+  inside = 0;
+  const V3 axis = G3(h, RH_AX);
+  const float rdota = (float)dot(ray, axis);
+  if (rdota == 0) return false;
+  const double sa = dot(start, axis);
+  const float t1 = (float)((h[RH_C1A] - sa) / rdota);
+  const float t2 = (float)((h[RH_C2A] - sa) / rdota);
+  if (t1 < eps && t2 < eps) return false;
+  if (t1 < eps || t2 < eps) {
+    inside = 1;
+    t = fmaxr(t1, t2);
+    return true;
+  }
+  t = fminr(t1, t2);
+  return true;
+}
+
+// RectPrismWithCylinder's slab test of its own bounds (geometry.cpp:1509-1592 / 1655-1734):
+// near-parallel axes (|ray| < 1e-4) take FLT_MIN/FLT_MAX when the start lies inside the slab
+// (closed interval for intersect, open for intersectShadow); false: missed
+template <bool SHADOW>
+__device__ __forceinline__ bool rpc_slab(GP g, V3 ray, V3 start, float& tmin_o, float& tmax_o)
+{
+  const float eps = 1e-4f;
+  const V3 inv = v3(1.0 / ray.x, 1.0 / ray.y, 1.0 / ray.z);
+  const V3 lb = G3(g, RP_LB), ub = G3(g, RP_UB);
+  float mn[3], mx[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double r = a == 0 ? ray.x : a == 1 ? ray.y : ray.z;
+    const double s = a == 0 ? start.x : a == 1 ? start.y : start.z;
+    const double l = a == 0 ? lb.x : a == 1 ? lb.y : lb.z, u = a == 0 ? ub.x : a == 1 ? ub.y : ub.z;
+    const double iv = a == 0 ? inv.x : a == 1 ? inv.y : inv.z;
+    if (fabs(r) < (double)eps) {
+      if (SHADOW ? !(s > l && s < u) : !(s >= l && s <= u)) return false;
+      mn[a] = FLT_MIN;
+      mx[a] = FLT_MAX;
+    } else if (r < 0) {
+      mn[a] = (float)((u - s) * iv);
+      mx[a] = (float)((l - s) * iv);
+    } else {
+      mn[a] = (float)((l - s) * iv);
+      mx[a] = (float)((u - s) * iv);
+    }
+  }
+  float tmin = mn[0], tmax = mx[0];
+  if (tmin > mx[1] || mn[1] > tmax) return false;
+  if (mn[1] > tmin) tmin = mn[1];
+  if (mx[1] < tmax) tmax = mx[1];
+  if (tmin > mx[2] || mn[2] > tmax) return false;
+  if (mn[2] > tmin) tmin = mn[2];
+  if (mx[2] < tmax) tmax = mx[2];
+  tmin_o = tmin;
+  tmax_o = tmax;
+  return true;
+}
+
+// RectPrismWithCylinder::intersect (geometry.cpp:1507-1651). t is the box's entry tmin (also when
+// the start lies inside, where the reference sets inside and then overwrites t = tmax with tmin).
+// The holes: the nearest body or cap-plane crossing; a cap crossing at or before the box entry
+// lets the ray through (false), a body hit there replaces t. The reference's uninitialised `hit` /
+// `cap_hit` are taken as false. It stores the hit hole's colour into the shape (sticky across later
+// rays, so the image depended on the render order); here it is the hit record's colour instead
+// (hcol: the hole colour's geom offset, -1: the prism colour).
+__device__ __forceinline__ bool rpc_hit(GP g, V3 ray, V3 start, float& t, int& inside, int& hcol)
+{
+  const float eps = 1e-4f;
+  float tmin, tmax;
+  inside = 0;
+  if (!rpc_slab<false>(g, ray, start, tmin, tmax)) return false;
+  if (tmax <= eps) return false;
+  if (tmin < eps && tmax > eps) inside = 1;
+  float tb = tmin;
+  float tcyl = FLT_MAX;
+  bool hit = false, cap_hit = false;
+  int ins_cyl = 0, hc = -1;
+  const int nh = (int)g[RP_NH];
+  for (int i = 0; i < nh; ++i) {
+    const int o = RP_H + i * RH_SIZE;
+    float tt;
+    int it = 0;
+    if (cyl_hit(g + o, ray, start, tt, it)) {
+      hit = true;
+      if (tt <= tcyl) { hc = o + RH_COL; ins_cyl = it; tcyl = tt; }
+    }
+    if (cyl_cap(g + o, ray, start, tt, it)) {
+      hit = true;
+      if (tt <= tcyl) { hc = o + RH_COL; cap_hit = true; ins_cyl = it; tcyl = tt; }
+    }
+  }
+  if (hit && tcyl <= tb) {
+    if (cap_hit) return false;
+    inside = ins_cyl;
+    tb = tcyl;
+    hcol = hc;
+  }
+  t = tb;
+  return true;
+}
+
+// RectPrismWithCylinder::intersectShadow (geometry.cpp:1653-1790): the box test ignores t_max
+// unless the start lies inside it (a box past the light occludes); a hole's cap crossing inside
+// (eps, t_max) at or before the box entry lets the ray through
+__device__ __forceinline__ bool rpc_shadow(GP g, V3 ray, V3 start, float t_max)
+{
+  const float eps = 1e-4f;
+  float tmin, tmax;
+  if (!rpc_slab<true>(g, ray, start, tmin, tmax)) return false;
+  if (tmax <= eps) return false;
+  if (tmin < eps && tmax > eps && tmax >= t_max) return false;
+  const float tb = tmin;
+  float tcyl = FLT_MAX;
+  bool hit = false, cap_hit = false;
+  const int nh = (int)g[RP_NH];
+  for (int i = 0; i < nh; ++i) {
+    const int o = RP_H + i * RH_SIZE;
+    float tt = FLT_MIN;
+    int it = 0;
+    if (cyl_hit(g + o, ray, start, tt, it) && tt > eps && tt < t_max) {
+      hit = true;
+      if (tt <= tcyl) tcyl = tt;
+    }
+    if (cyl_cap(g + o, ray, start, tt, it) && tt > eps && tt < t_max) {
+      hit = true;
+      if (tt <= tcyl) { cap_hit = true; tcyl = tt; }
+    }
+  }
+  if (hit && tcyl <= tb && tcyl > eps && tcyl < t_max && cap_hit) return false;
+  return true;
+}
+
+#endif  // DT_WITH_RPC
+
 // Moller-Trumbore (geometry.cpp:488-586); returns 0 miss, else writes t_final
 __device__ __forceinline__ bool tri_core(GP g, V3 ray, V3 start, float& t_final)
 {
@@ -653,6 +805,10 @@ __device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, GP
       if (tmin < FLT_MAX) { t = tmin; return true; }
       return false;
     }
+#if DT_WITH_RPC
+    case DT_SHAPE_RECTPRISM_CYL:
+      return rpc_hit(g, ray, start, t, inside, ccol);
+#endif
     case DT_SHAPE_CHECKERBOARD:
     case DT_SHAPE_CHECKERBOARD_HOLE: {
       inside = 0;
@@ -725,6 +881,10 @@ __device__ bool shape_shadow(int type, uint32_t flags, GP g, V3 ray, V3 start,
       for (int f = 0; f < 6; ++f)
         if (rect_hit_R(g + PR_F + f * R_SIZE, ray, start, 1e-4f, tt, a, b, t_max) && tt < t_max) return true;
       return false;
+#if DT_WITH_RPC
+    case DT_SHAPE_RECTPRISM_CYL:
+      return rpc_shadow(g, ray, start, t_max);
+#endif
     case DT_SHAPE_CHECKERBOARD_HOLE:
       if (rect_hit_R(g + CK_R, ray, start, 1e-3f, tt, a, b, t_max) && tt < t_max) {
         if (rect_hit_R(g + CK_HOLE, ray, start, 1e-4f, tt, a, b, t_max) && tt < t_max) return false;
@@ -735,11 +895,32 @@ __device__ bool shape_shadow(int type, uint32_t flags, GP g, V3 ray, V3 start,
   return false;
 }
 
-// GeoPrimitive::getNorm (per-lane shape index)
+// GeoPrimitive::getNorm (per-lane shape index); ccol: the hit record's colour offset (a
+// RectPrismWithCylinder hole: its record is at ccol - RH_COL)
 __device__ __forceinline__ V3 shape_norm(int type, uint32_t flags, GP g, V3 p, float shift,
-                         unsigned long long* st_prism)
+                         unsigned long long* st_prism, int ccol)
 {
   switch (type) {
+#if DT_WITH_RPC
+    case DT_SHAPE_RECTPRISM_CYL: {
+      // RectPrismWithCylinder::getNorm (geometry.cpp:1792-1821): lastHit is always -1 here (intersect
+      // resets it before every `return true`), so the face tests below decide, signed and unnormalised
+      const float eps = 1e-3f;
+      const V3 pa = sub(p, G3(g, RP_A));
+      if (dot(pa, G3(g, RP_NBOT)) <= eps) return G3(g, RP_NBOT);
+      if (dot(pa, G3(g, RP_NRIGHT)) <= eps) return G3(g, RP_NRIGHT);
+      if (dot(pa, G3(g, RP_NFRONT)) <= eps) return G3(g, RP_NFRONT);
+      // the reference throws ("point is not on prism", 1819-1820): counted; the hit hole's normal
+      // (Cylinder::getNorm, 419-425), else the front normal
+      atomicAdd(st_prism, 1ull);
+      if (ccol >= 0) {
+        const int h = ccol - RH_COL;
+        const V3 axis = G3(g, h + RH_AX), pc = sub(p, G3(g, h + RH_C1));
+        return normalized(sub(pc, mul(dot(pc, axis), axis)));
+      }
+      return G3(g, RP_NFRONT);
+    }
+#endif
     case DT_SHAPE_SPHERE: {
       V3 n = sub(p, G3(g, SP_C));
       return divs(n, norm(n));
@@ -802,6 +983,18 @@ __device__ __forceinline__ int shape_uv(int type, uint32_t flags, GP g, V3 p, fl
       vo = (float)(norm(cross(sub(p, D), dc)) / nadc);
       return 1;
     }
+#if DT_WITH_RPC
+    case DT_SHAPE_RECTPRISM_CYL: {
+      // RectPrism::getUV (geometry.cpp:1442-1461): valid only where |(ad x dc).p| <= 1e-5
+      if (fabs(dot(G3(g, RP_ADC), p)) <= 1e-5) {
+        uo = (float)(norm(cross(sub(p, G3(g, RP_A)), G3(g, RP_AD))) / g[RP_NADC]);
+        vo = (float)(norm(cross(sub(p, G3(g, RP_D)), G3(g, RP_DC))) / g[RP_NADC]);
+        return 1;
+      }
+      uo = -1; vo = -1;
+      return 0;
+    }
+#endif
     case DT_SHAPE_RECTPRISM_V2: {
       V3 A = G3(g, PR_F + R_A), ad = G3(g, PR_AD), dc = G3(g, PR_DC), D = G3(g, PR_D);
       uo = (float)(norm(cross(sub(p, A), ad)) / g[PR_NADC]);
@@ -1071,10 +1264,12 @@ __device__ __forceinline__ bool bump_leaf_gathered(const DScene& S, const Walk& 
   return ok;
 }
 
-// every active lane's motion-blur shift lies within the bump tree's padding
+// every active lane's motion-blur shift lies within the bump tree's padding, and is >= 0 when the
+// tree (and the blur-padded grid lists) were padded for non-negative shifts only (host_accel.cpp):
+// the render's globals may draw shifts the build's did not
 __device__ __forceinline__ bool bump_tree_ok(const DParams& P, bool active, float shift)
 {
-  return P.n_bnodes > 0 && !__ballot(active && !(fabsf(shift) <= P.bump_pad));
+  return P.n_bnodes > 0 && !__ballot(active && !(fabsf(shift) <= P.bump_pad && (shift >= 0.0f || !P.bump_up_only)));
 }
 
 // closest hit over the lanes with `active` (cpp:491-538)
@@ -1107,7 +1302,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
     // failed an ancestor fails here too (host_fasttree.cpp)
     const bool act = GENERAL ? resume <= i : active;
 #if !DT_TCULL_HOIST
-    tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
+    tcull = (h.t_min == FLT_MAX || (DT_WITH_RPC && P.no_cull)) ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
 #endif
     bool hb = act & node_hit<GENERAL>(w, nd, shift, org, tcull);
     DT_WORK(cnt.wnodes++; cnt.box += act);
@@ -1303,7 +1498,7 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
   const DNodeDev* const NODES = BUMP ? S.bnodes : ftree ? S.fnodes : S.nodes;   // any-hit: order free
   int resume = active ? 0 : 0x7fffffff;
   bool occl = false;
-  const float tcull = shadow_tcull(t_max);
+  const float tcull = (DT_WITH_RPC && P.no_cull) ? FLT_MAX : shadow_tcull(t_max);
 #ifdef DT_ABL_NOSHADOW
   return false;
 #endif
@@ -1432,7 +1627,8 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift)))
     return occluded_walk<1>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
   // blur passes use the grid when its lists were built for their shifts (sg_ypad)
-  const bool bump_list = w.bump_wave && P.sg_ypad >= P.bump_pad;
+  // (umbra cells are only proven for shifts >= 0: with symmetric padding blur waves walk the tree)
+  const bool bump_list = w.bump_wave && P.sg_ypad >= P.bump_pad && P.bump_up_only;
   if (w.bump_wave && !bump_list) return occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 #ifdef DT_ABL_NOSHADOW
   return false;
@@ -1779,7 +1975,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       GP g = cas(S.geom) + hd.off;
       const DMat& M = S.mat[sid];
       isectP = add(eye, mul(h.t_min, ray));
-      normal = shape_norm(hd.type, hd.flags, g, isectP, shift, S.stats + ST_PRISM);
+      normal = shape_norm(hd.type, hd.flags, g, isectP, shift, S.stats + ST_PRISM, h.ccol);
       in = normalized(ray);
       shape_color = h.ccol >= 0 ? G3(g, h.ccol) : v3a(M.color);
       out.in_motion = (M.flags & DT_F_MOTION) != 0;
@@ -2155,7 +2351,7 @@ struct DLaunch {
 #define DT_TRACE_MIN_WAVES 1
 #endif
 extern "C" __global__ void __launch_bounds__(64, DT_TRACE_MIN_WAVES)
-dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
+DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
 {
   const DScene& S = Lp->S;
   const DParams& P = Lp->P;
@@ -2357,6 +2553,7 @@ dt_trace_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   }
 }
 
+#if !DT_WITH_RPC
 // The sky of the pixels a 1-spp trace launch flagged as missed (P.sky_defer): renderImage's miss
 // branch (cpp:1074-1092: cloudColor of mcam * focalPoint) one pixel per lane, at the occupancy of a
 // small kernel instead of inside the trace kernel's register budget. With one sample the pixel is
@@ -2481,3 +2678,11 @@ extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_
   return hipGetLastError();
 }
 extern "C" const void* dt_trace_kernel_ptr(void) { return (const void*)dt_trace_kernel; }
+#else   // DT_WITH_RPC: the trace kernel for scenes with a RectPrismWithCylinder
+extern "C" hipError_t dt_launch_trace_rpc(const void* dev_launch, float* out, int grid, hipStream_t stream)
+{
+  hipLaunchKernelGGL(dt_trace_kernel_rpc, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
+  return hipGetLastError();
+}
+extern "C" const void* dt_trace_kernel_rpc_ptr(void) { return (const void*)dt_trace_kernel_rpc; }
+#endif

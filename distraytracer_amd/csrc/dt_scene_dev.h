@@ -97,6 +97,16 @@ enum { CK_R = 0, CK_GN = 14, CK_A = 17, CK_B = 20, CK_C = 23, CK_D = 26, CK_HOLE
        CK_COL1 = 44, CK_COL2 = 47, CK_COL = 50, CK_AD = 53, CK_DC = 56, CK_NADC = 59, CK_MUD = 60,
        CK_MVD = 61, CK_BW = 62, CK_SIZE = 63 };
 
+// RECTPRISM_CYL (RectPrismWithCylinder, geometry.cpp:1467-1821): the box's own bounds
+// (RectPrism::getBounds of the 8 vertices, used by its slab-test intersect), getNorm's normals
+// (1802-1804) and A, RectPrism::getUV's block (1442-1461: ad = D-A, dc = C-D, ad x dc,
+// |ad||dc|, D), the hole count, then one record per hole (Cylinder, geometry.cpp:227-240):
+// c1, c2, axis, r2 at the CYLINDER offsets (CY_C1..CY_R2, so the cylinder tests take a hole
+// record as is), its colour, and c1.axis, c2.axis of intersectCap (297-324)
+enum { RP_LB = 0, RP_UB = 3, RP_NBOT = 6, RP_NRIGHT = 9, RP_NFRONT = 12, RP_A = 15, RP_AD = 18, RP_DC = 21,
+       RP_ADC = 24, RP_NADC = 27, RP_D = 30, RP_NH = 33, RP_H = 34 };
+enum { RH_C1 = 0, RH_C2 = 3, RH_AX = 6, RH_R2 = 9, RH_COL = 10, RH_C1A = 13, RH_C2A = 14, RH_SIZE = 15 };
+
 #define DT_MAX_SGRID 16        // lights with a shadow grid (host_shadowgrid.cpp)
 #define DT_SGRID_MAX_LIST 96   // longer candidate lists: the cell walks the tree instead
 #define DT_SG_REACH_DEFAULT 0.25f   // a cell's list covers points this many cells outside it
@@ -133,6 +143,11 @@ struct DParams {
   int32_t prio_steps;     // DFS steps after which a wave raises its issue priority (0: never)
   int32_t ls_first;       // first area (rectangle) light: where the light-sample cache starts
   int32_t sky_defer;      // 1 spp: missed pixels are flagged, dt_sky_miss_kernel marches them per lane
+  int32_t no_cull;        // 1: no t-culling of boxes (closest hit past the best t, shadow past the light):
+                          // a RectPrismWithCylinder occludes beyond the light and its hole can be hit
+                          // outside its box (host: no shadow grid, no primary lists either)
+  int32_t bump_up_only;   // the bump tree / blur-padded lists were built for shifts >= 0 only (host_accel.cpp):
+                          // a lane with a negative shift sends its wave to the reference-tree walk
   uint32_t seed;
   float aperture, focal_length, near_plane;
   float l, r, t, b;

@@ -1,7 +1,8 @@
 // dtrender — host CLI mirroring the reference's `./render` modes (render_final_project.cpp:
 // 1386-1956) on top of the C-ABI: builds the scene with the host builders, renders on the
-// current MI355X through libdt's HIP kernels, writes the PPM. Models and ./ads assets are
-// absent, so use_model is forced off and tunnel frames report DT_E_UNSUPPORTED.
+// current MI355X through libdt's HIP kernels, writes the PPM. The models and ./ads assets are
+// absent: use_model is off, and the tunnel's ad frames are the procedural stand-ins
+// of host_scenes.cpp.
 //
 //   dtrender                 default: 980x540, antialias 2, frame 30 -> buildFinal(240) (1410-1424)
 //   dtrender final <n>       1920x1080, antialias 10, depth 10, buildFinal(n*8) (1446-1456)
@@ -9,6 +10,7 @@
 //   dtrender nodistr <n>     antialias 6 (1457-1469)
 //   dtrender perlin <i>      renderImageCloud 640x480 (1685-1698)
 //   dtrender spheres         buildSceneSpheres(0) 256x256 (config C1)
+//   dtrender prismcyl <n>    BuildScenePrismCylinder(n) 640x480 (1711-1723)
 // options (after the mode): --out FILE(.ppm|.png)  --spp N  --depth N  --res WxH  --seed S
 #include <cmath>
 #include <cstdio>
@@ -79,6 +81,11 @@ int main(int argc, char** argv)
   } else if (mode == "spheres") {
     scene = "spheres";
     snprintf(buf, sizeof buf, "./spheres.ppm");
+  } else if (mode == "prismcyl") {
+    scene = "prismcyl";
+    g.xRes = 640; g.yRes = 480;
+    frame = arg; build_frame = (float)arg;
+    snprintf(buf, sizeof buf, "./test_frames/prismcyl/frame.%04d.ppm", arg);
   } else {
     fprintf(stderr, "unknown mode %s\n", mode.c_str());
     return 2;

@@ -102,13 +102,20 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
   if (a.bnodes.empty()) a.bnodes.push_back(dnodes.empty() ? dtd::DNodeDev() : dnodes[0]);
   if (a.bparent.empty()) a.bparent.push_back(-1);
   stage("bump tree");
+  // RectPrismWithCylinder (geometry.cpp:1653-1790) reports a shadow hit wherever the ray's line
+  // crosses its box ahead of the start, past the light included, and a hit on one of its holes can
+  // lie outside its box: the exactness arguments of t-culling, of the shadow grid and of the
+  // primary lists (an occluder lies on the segment, a hit inside its leaf box) do not hold for it.
+  // A scene that holds one walks the trees without culling (DParams::no_cull).
+  for (const dtd::DShapeHdr& h : f.hdr)
+    if (h.type == DT_SHAPE_RECTPRISM_CYL) a.no_cull = true;
   // shadow grid (host_shadowgrid.cpp); DT_SHADOW_GRID=0: every shadow test walks a tree.
   // Reach 0.25 cells and lists of up to 96 leaves (round 1: 0.5, 48): C3 +0.6%, C2 +0.5%, C4 +0.2%,
   // C5 transition frame 1088 -9%, tunnel frames -2% (profiles/r02bj_ab_reach_cap.log)
   const char* sgv = getenv("DT_SHADOW_GRID");
   const char* sgc = getenv("DT_SG_CELLS");
   const char* sgr = getenv("DT_SG_REACH");
-  if ((sgv && sgv[0] == '0') ||
+  if ((sgv && sgv[0] == '0') || a.no_cull ||
       !build_shadow_grid(dnodes, f, a.sg, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : DT_SG_REACH_DEFAULT,
                          a.n_bnodes > 0 ? (double)a.bump_pad : 0.0, up_only))
     a.sg = ShadowGrid();

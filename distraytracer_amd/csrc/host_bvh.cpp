@@ -191,7 +191,8 @@ void shape_bounds(const dt_shape_desc& sh, V3& lb, V3& ub)
       return;
     }
     default: {  // Triangle 596-602, Rectangle 761-770, RectPrismV2 922-941
-      int n = sh.type == DT_SHAPE_TRIANGLE ? 3 : (sh.type == DT_SHAPE_RECTPRISM_V2 ? 8 : 4);
+      // RectPrismV2 / RectPrismWithCylinder (RectPrism::getBounds, geometry.cpp:922-941, 1382-1401): 8 vertices
+      int n = sh.type == DT_SHAPE_TRIANGLE ? 3 : ((sh.type == DT_SHAPE_RECTPRISM_V2 || sh.type == DT_SHAPE_RECTPRISM_CYL) ? 8 : 4);
       V3 mn = cmin(v3a(sh.v[0]), v3a(sh.v[1])), mx = cmax(v3a(sh.v[0]), v3a(sh.v[1]));
       for (int k = 2; k < n; ++k) {
         mn = cmin(mn, v3a(sh.v[k]));

@@ -58,6 +58,10 @@ int flatten_scene(const dt_scene_desc& d, const dt_globals& g, FlatScene& out, s
     err = "invalid scene descriptor";
     return DT_E_INVALID;
   }
+  if (d.n_holes < 0 || (d.n_holes > 0 && !d.holes)) {
+    err = "invalid hole array";
+    return DT_E_INVALID;
+  }
   if (d.n_lights > 32) {   // the device keeps one visibility bit per light in a 32-bit mask
     err = "more than 32 lights";
     return DT_E_LIMIT;
@@ -173,6 +177,45 @@ int flatten_scene(const dt_scene_desc& d, const dt_globals& g, FlatScene& out, s
         put3(G, at + dtd::PR_D, D);
         break;
       }
+      case DT_SHAPE_RECTPRISM_CYL: {
+        // RectPrismWithCylinder (geometry.cpp:1467-1505) and its holes (Cylinder ctor, 227-240)
+        if (s.n_holes < 0 || (s.n_holes > 0 && (!d.holes || s.hole_first < 0 || s.hole_first + s.n_holes > d.n_holes))) {
+          err = "shape " + std::to_string(i) + ": hole range out of the descriptor's holes";
+          return DT_E_INVALID;
+        }
+        G.resize(at + dtd::RP_H + (size_t)s.n_holes * dtd::RH_SIZE, 0.0);
+        V3 lb, ub;
+        shape_bounds(s, lb, ub);   // RectPrism::getBounds (1382-1401), the box intersect tests
+        put3(G, at + dtd::RP_LB, lb);
+        put3(G, at + dtd::RP_UB, ub);
+        V3 A = VV(s, 0), B = VV(s, 1), C = VV(s, 2), D = VV(s, 3), E = VV(s, 4), F = VV(s, 5), H = VV(s, 7);
+        // getNorm (1802-1804)
+        put3(G, at + dtd::RP_NBOT, neg(normalized(cross(sub(F, E), sub(H, E)))));
+        put3(G, at + dtd::RP_NRIGHT, normalized(cross(sub(E, A), sub(D, A))));
+        put3(G, at + dtd::RP_NFRONT, normalized(cross(sub(B, A), sub(E, A))));
+        put3(G, at + dtd::RP_A, A);
+        V3 ad = sub(D, A), dc = sub(C, D);   // RectPrism::getUV (1445-1453)
+        put3(G, at + dtd::RP_AD, ad);
+        put3(G, at + dtd::RP_DC, dc);
+        put3(G, at + dtd::RP_ADC, cross(ad, dc));
+        G[at + dtd::RP_NADC] = norm(ad) * norm(dc);
+        put3(G, at + dtd::RP_D, D);
+        G[at + dtd::RP_NH] = s.n_holes;
+        for (int k = 0; k < s.n_holes; ++k) {
+          const dt_shape_desc& hs = d.holes[s.hole_first + k];
+          const size_t o = at + dtd::RP_H + (size_t)k * dtd::RH_SIZE;
+          V3 c1 = VV(hs, 0), c2 = VV(hs, 1);
+          V3 axis = normalized(sub(c2, c1));
+          put3(G, o + dtd::RH_C1, c1);
+          put3(G, o + dtd::RH_C2, c2);
+          put3(G, o + dtd::RH_AX, axis);
+          G[o + dtd::RH_R2] = pow((double)hs.radius, 2.0);   // pow(radius, 2) (250)
+          put3(G, o + dtd::RH_COL, v3a(hs.color));
+          G[o + dtd::RH_C1A] = dot(c1, axis);   // c1.dot(axis) of intersectCap (307)
+          G[o + dtd::RH_C2A] = dot(c2, axis);   // c2.dot(axis) (308)
+        }
+        break;
+      }
       case DT_SHAPE_CHECKERBOARD:
       case DT_SHAPE_CHECKERBOARD_HOLE: {
         G.resize(at + dtd::CK_SIZE, 0.0);
@@ -212,7 +255,8 @@ int flatten_scene(const dt_scene_desc& d, const dt_globals& g, FlatScene& out, s
     if (s.flags & DT_F_TEXTURE) {
       if (s.tex_frame < 0 || s.tex_frame >= d.n_textures) {
         if (s.type == DT_SHAPE_RECTANGLE || s.type == DT_SHAPE_RECTPRISM_V2 || s.type == DT_SHAPE_TRIANGLE ||
-            s.type == DT_SHAPE_CHECKERBOARD_HOLE || s.type == DT_SHAPE_CHECKER_CYLINDER) {
+            s.type == DT_SHAPE_CHECKERBOARD_HOLE || s.type == DT_SHAPE_CHECKER_CYLINDER ||
+            s.type == DT_SHAPE_RECTPRISM_CYL) {
           err = "shape " + std::to_string(i) + ": texture index out of range";
           return DT_E_INVALID;
         }

@@ -111,6 +111,7 @@ struct Accel {
   int n_fnodes = 0, n_bnodes = 0;
   float bump_pad = 0;
   bool bump_up_only = false;           // every blur shift >= 0 (blur_leaf_pad)
+  bool no_cull = false;                // a RectPrismWithCylinder: no t-culling, no shadow grid (DParams::no_cull)
   int ftree_mode = 0;
   int boxes_ordered = 0;
   ShadowGrid sg;

@@ -28,15 +28,18 @@ struct OwnedDesc {
   std::vector<dt_light_desc> lights;
   std::vector<dt_texture_desc> tex;
   std::vector<std::vector<uint8_t>> texdata;
+  std::vector<dt_shape_desc> holes;   // RectPrismWithCylinder::holes of the scene's prisms
   void finish()
   {
     d.n_shapes = (int32_t)shapes.size();
     d.n_lights = (int32_t)lights.size();
     d.n_textures = (int32_t)tex.size();
+    d.n_holes = (int32_t)holes.size();
     for (size_t i = 0; i < tex.size(); ++i) tex[i].pixels = texdata[i].data();
     d.shapes = shapes.empty() ? nullptr : shapes.data();
     d.lights = lights.empty() ? nullptr : lights.data();
     d.textures = tex.empty() ? nullptr : tex.data();
+    d.holes = holes.empty() ? nullptr : holes.data();
   }
 };
 
@@ -145,6 +148,17 @@ dt_shape_desc RectPrismV2(V3 a, V3 b, V3 c, V3 d, V3 e, V3 f, V3 g, V3 h, V3 col
   for (int k = 1; k < 8; ++k) ctr = add(ctr, vv[k]);
   set3(s.center, divs(ctr, 8));
   if (texframe >= 0) s.tex_frame = texframe;
+  return s;
+}
+
+// RectPrismWithCylinder(a..h, col, material, in_motion, texframe, shader)  geometry.cpp:1467-1505;
+// its holes are appended to O.holes by the caller (tmp->holes.push_back, scene.h:3241)
+dt_shape_desc RectPrismWithCylinder(V3 a, V3 b, V3 c, V3 d, V3 e, V3 f, V3 g, V3 h, V3 col,
+                                    const std::string& material = "", bool motion = false, int texframe = -1,
+                                    const std::string& shader = "lambert")
+{
+  dt_shape_desc s = RectPrismV2(a, b, c, d, e, f, g, h, col, material, motion, texframe, shader);
+  s.type = DT_SHAPE_RECTPRISM_CYL;   // same vertex members, centre (A+..+H)/8 and float length/width
   return s;
 }
 
@@ -592,6 +606,48 @@ int build_hw4(float, dt_globals&, OwnedDesc& O)
   return DT_OK;
 }
 
+// ---- BuildScenePrismCylinder (scene.h:3227-3263), the `./render prismcyl` mode ----------------
+// A 4x4x1 box (RectPrismWithCylinder) with one cylinder hole of radius 1 through it, a point light;
+// the eye is rotated about itself (to_origin, rotation, from_origin around og_eye), which leaves it
+// at og_eye up to the rounding of the 4x4 products (sequential sums, oracle.c header).
+int build_prismcyl(float frame, dt_globals& g, OwnedDesc& O)
+{
+  const V3 A = v3(0, -2, -2), B = v3(0, -2, 2), C = v3(0, 2, 2), D = v3(0, 2, -2), back = v3(1, 0, 0);
+  dt_shape_desc p = RectPrismWithCylinder(A, B, C, D, add(A, back), add(B, back), add(C, back), add(D, back),
+                                          v3(1, 0, 0));
+  const V3 c1 = divs(add(add(add(A, B), C), D), 4);
+  const V3 c2 = add(c1, back);
+  p.hole_first = (int32_t)O.holes.size();
+  p.n_holes = 1;
+  O.holes.push_back(Cylinder(c1, c2, 1, v3(0, 0, 1)));
+  O.shapes.push_back(p);
+  PointLight(O, v3(-5, 1, 0), v3(1, 1, 1));
+  const double og[4] = {-6, 0.5, 1, 1};
+  const float theta = (float)(M_PI * 2 * frame / 50);
+  // cos(theta) / sin(theta) of a float: <cmath>'s float overloads (cosf / sinf)
+  const double ct = cosf(theta), st = sinf(theta);
+  const double to_origin[4][4] = {{1, 0, 0, -og[0]}, {0, 1, 0, -og[1]}, {0, 0, 1, -og[2]}, {0, 0, 0, 1}};
+  const double rot[4][4] = {{ct, 0, st, 0}, {0, 1, 0, 0}, {-st, 0, ct, 0}, {0, 0, 0, 1}};
+  const double from_origin[4][4] = {{1, 0, 0, og[0]}, {0, 1, 0, og[1]}, {0, 0, 1, og[2]}, {0, 0, 0, 1}};
+  double m1[4][4], m2[4][4];
+  auto mul4 = [](const double a[4][4], const double b[4][4], double r[4][4]) {
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) {
+        double acc = a[i][0] * b[0][j];
+        for (int k = 1; k < 4; ++k) acc = acc + a[i][k] * b[k][j];
+        r[i][j] = acc;
+      }
+  };
+  mul4(from_origin, rot, m1);
+  mul4(m1, to_origin, m2);
+  for (int i = 0; i < 3; ++i) {
+    double acc = m2[i][0] * og[0];
+    for (int k = 1; k < 4; ++k) acc = acc + m2[i][k] * og[k];
+    g.eye[i] = acc;
+  }
+  return DT_OK;
+}
+
 // bone table written by tools/gen_bones.py from dt_mocap_bone_table
 bool load_bones(const std::string& data_dir, int posture_frame, std::vector<double>& out, std::string& err)
 {
@@ -898,6 +954,7 @@ extern "C" int dt_build_scene(const char* name, float frame, dt_globals* g, cons
   if (n == "spheres") rc = build_spheres(frame, *g, *O);
   else if (n == "dof") rc = build_dof(frame, *g, *O);
   else if (n == "hw4") rc = build_hw4(frame, *g, *O);
+  else if (n == "prismcyl") rc = build_prismcyl(frame, *g, *O);
   else if (n == "final") rc = build_final(frame, *g, dir, *O, err);
   else {
     err = "unknown scene " + n;

@@ -32,8 +32,13 @@ class FrameSplit:
         parts = list(gathered.view(self.world, self.slab_floats).unbind(0)) if self.rank == 0 else None
         return dist.gather(slab, gather_list=parts, dst=0, group=group, async_op=async_op)
 
-    def assemble(self, gathered, image):
-        unpack_slabs(self.g, self.base, self.world, gathered, image)
+    def assemble(self, gathered, image, stream=None):
+        """scatter the gathered slabs into the ppmOut image; on the GPU the unpack kernel runs on
+        `stream` (default: torch's current stream, the one the gather's wait() ordered)"""
+        if stream is None and getattr(gathered, "is_cuda", False):
+            import torch
+            stream = torch.cuda.current_stream(gathered.device).cuda_stream
+        unpack_slabs(self.g, self.base, self.world, gathered, image, stream=stream)
 
 
 class GatherPipeline:
@@ -62,6 +67,6 @@ class GatherPipeline:
             return
         work, b = self.pending
         self.pending = None
-        work.wait()
+        work.wait()   # orders torch's current stream after the collective
         if self.split.rank == 0:
-            self.split.assemble(self.gathered[b], self.image)
+            self.split.assemble(self.gathered[b], self.image)   # on that same stream

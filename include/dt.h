@@ -36,7 +36,10 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 1
+/* 2: dt_tiles ownership by hashed tile groups (dtd::tile_of) with equal-size slabs,
+ *    dt_scene_prepare / dt_scene_upload / dt_accel_info_build, RectPrismWithCylinder
+ *    (DT_SHAPE_RECTPRISM_CYL with the dt_scene_desc.holes array) */
+#define DT_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------- */
 #define DT_OK              0
@@ -56,7 +59,9 @@ enum dt_shape_type {
   DT_SHAPE_RECTPRISM_V2     = 5, /* RectPrismV2       geometry.cpp:784-948  */
   DT_SHAPE_CHECKERBOARD     = 6, /* Checkerboard      geometry.cpp:2248-2341 */
   DT_SHAPE_CHECKERBOARD_HOLE= 7, /* CheckerboardWithHole geometry.cpp:2344-2561 */
-  DT_SHAPE_CHECKER_CYLINDER = 8  /* CheckerCylinder   geometry.cpp:2563-2630 */
+  DT_SHAPE_CHECKER_CYLINDER = 8, /* CheckerCylinder   geometry.cpp:2563-2630 */
+  DT_SHAPE_RECTPRISM_CYL    = 9  /* RectPrismWithCylinder geometry.cpp:1467-1821 (axis-aligned
+                                    box of the 8 vertices with cylinder holes; holes[] below) */
 };
 
 /* GeoPrimitive::model (render_final_project.cpp:894-948) */
@@ -115,10 +120,14 @@ typedef struct dt_shape_desc {
    *   TRIANGLE          v[0..2] = A,B,C
    *   RECTANGLE / CHECKERBOARD     v[0..3] = A,B,C,D
    *   RECTPRISM_V2      v[0..7] = A..H
-   *   CHECKERBOARD_HOLE v[0..3] = A,B,C,D ; v[4..7] = hole rectangle A,B,C,D */
+   *   CHECKERBOARD_HOLE v[0..3] = A,B,C,D ; v[4..7] = hole rectangle A,B,C,D
+   *   RECTPRISM_CYL     v[0..7] = A..H ; holes: dt_scene_desc.holes[hole_first ..
+   *                     hole_first + n_holes) (RectPrismWithCylinder::holes, geometry.h:196) */
   double   v[8][3];
   double   mesh_normal[3];
   double   uv[3][2];    /* Triangle uvA, uvB, uvC */
+  int32_t  hole_first;  /* RECTPRISM_CYL: first entry in dt_scene_desc.holes */
+  int32_t  n_holes;     /* RECTPRISM_CYL: number of holes (0 for every other type) */
 } dt_shape_desc;
 
 /* ---- lights (geometry.h:279-307, geometry.cpp:2745-2849) ---------------- */
@@ -158,6 +167,11 @@ typedef struct dt_scene_desc {
   const dt_shape_desc*   shapes;
   const dt_light_desc*   lights;
   const dt_texture_desc* textures;
+  /* Cylinder holes of RECTPRISM_CYL shapes (type CYLINDER records: v[0] = c1, v[1] = c2, radius,
+   * color; geometry.cpp:227-240). They are not shapes of the scene: only their prism tests them. */
+  int32_t                n_holes;
+  int32_t                _pad2;
+  const dt_shape_desc*   holes;
 } dt_scene_desc;
 
 /* ---- globals (render_final_project.cpp:48-137) -------------------------- */
@@ -211,7 +225,8 @@ typedef struct dt_stats {
   uint64_t uv_out_of_range;   /* reference terminates here (cpp:870-877), we count */
   uint64_t glossy_exhausted;  /* >10 invalid glossy resamples (cpp:724-740)      */
   uint64_t spherelight_exhausted; /* geometry.cpp:2785-2789                      */
-  uint64_t prism_norm_fallback;   /* RectPrismV2::getNorm off-surface (geometry.cpp:895) */
+  uint64_t prism_norm_fallback;   /* RectPrismV2::getNorm off-surface (geometry.cpp:895);
+                                     RectPrismWithCylinder::getNorm's throw (geometry.cpp:1819-1820) */
   uint64_t reflect_errors;    /* refl.n <= 0 (cpp:631-638)                       */
   uint64_t nan_pixels;
   uint64_t tex_fetches;       /* texel reads (algorithmic bytes) */
@@ -303,7 +318,8 @@ int dt_unpack_slabs(const dt_globals* g, const dt_tiles* tiles, int32_t world,
 
 /* ---- host scene builders (scene.h) ---------------------------------------- */
 /* name: "final" (buildFinal scene.h:605), "spheres" (buildSceneSpheres 4399),
- * "dof" (buildSceneDOF 4422), "hw4" (buildSceneHW4 4451).
+ * "dof" (buildSceneDOF 4422), "hw4" (buildSceneHW4 4451), "prismcyl"
+ * (BuildScenePrismCylinder 3227, the `./render prismcyl` mode, cpp:1711-1723).
  * Mutates g exactly as the reference builder mutates its globals (Q23, fresh-process
  * semantics: call dt_globals_default first for a fresh frame).
  * data_dir holds textures/<name>.rgb and bones_<motion>.bin. */

@@ -599,15 +599,200 @@ static V3 checker_color(const dt_shape_desc* sh, float check1, float check2)
   return color;
 }
 
+/* ---- RectPrismWithCylinder (geometry.cpp:1467-1821) -------------------------------------- */
+/* RectPrism::getBounds (1382-1401), used by the constructor for the box the tests slab */
+static void rpc_bounds(const dt_shape_desc* sh, V3* lb, V3* ub)
+{
+  V3 mn = cmin(v3a(sh->v[0]), v3a(sh->v[1])), mx = cmax(v3a(sh->v[0]), v3a(sh->v[1]));
+  for (int k = 2; k < 8; ++k) { mn = cmin(mn, v3a(sh->v[k])); mx = cmax(mx, v3a(sh->v[k])); }
+  *lb = mn;
+  *ub = mx;
+}
+
+/* Cylinder::intersectCap (297-324): both cap planes, no radius test */
+static int cyl_intersect_cap(const dt_shape_desc* cyl, V3 ray, V3 start, float* t, int* inside)
+{
+  float eps = 1e-3f;
+  *inside = 0;
+  V3 c1 = v3a(cyl->v[0]), c2 = v3a(cyl->v[1]), axis = cyl_axis(cyl);
+  float rdota = (float)dot(ray, axis);
+  if (rdota == 0) return 0;
+  float t1 = (float)((dot(c1, axis) - dot(start, axis)) / rdota);
+  float t2 = (float)((dot(c2, axis) - dot(start, axis)) / rdota);
+  if (t1 < eps && t2 < eps) return 0;
+  else if (t1 < eps || t2 < eps) { *inside = 1; *t = fmaxr(t1, t2); return 1; }
+  *t = fminr(t1, t2);
+  return 1;
+}
+
+/* the per-axis part of the box slab test (1515-1533 and the y/z copies): 0 = miss */
+static int rpc_axis(double r, double s, double l, double u, double inv, int open_interval, float* mn, float* mx)
+{
+  float eps = 1e-4f;
+  if (fabs(r) < eps) {
+    int in = open_interval ? (s > l && s < u) : (s >= l && s <= u);
+    if (!in) return 0;
+    *mn = FLT_MIN;
+    *mx = FLT_MAX;
+  } else if (r < 0) {
+    *mn = (float)((u - s) * inv);
+    *mx = (float)((l - s) * inv);
+  } else {
+    *mn = (float)((l - s) * inv);
+    *mx = (float)((u - s) * inv);
+  }
+  return 1;
+}
+
+/* the box's slab sequence (1511-1588 / 1657-1734); 0 = miss */
+static int rpc_box(const dt_shape_desc* sh, V3 ray, V3 start, int open_interval, float* tmin_o, float* tmax_o)
+{
+  V3 lb, ub;
+  rpc_bounds(sh, &lb, &ub);
+  V3 inv_ray = v3(1.0 / ray.x, 1.0 / ray.y, 1.0 / ray.z);   /* ray.cwiseInverse() */
+  float tmin, tmax, tymin, tymax, tzmin, tzmax;
+  if (!rpc_axis(ray.x, start.x, lb.x, ub.x, inv_ray.x, open_interval, &tmin, &tmax)) return 0;
+  if (!rpc_axis(ray.y, start.y, lb.y, ub.y, inv_ray.y, open_interval, &tymin, &tymax)) return 0;
+  if (tmin > tymax || tymin > tmax) return 0;
+  if (tymin > tmin) tmin = tymin;
+  if (tymax < tmax) tmax = tymax;
+  if (!rpc_axis(ray.z, start.z, lb.z, ub.z, inv_ray.z, open_interval, &tzmin, &tzmax)) return 0;
+  if (tmin > tzmax || tzmin > tmax) return 0;
+  if (tzmin > tmin) tmin = tzmin;
+  if (tzmax < tmax) tmax = tzmax;
+  *tmin_o = tmin;
+  *tmax_o = tmax;
+  return 1;
+}
+
+/* RectPrismWithCylinder::intersect (1507-1651). The reference's `hit` and `cap_hit` are
+ * uninitialised: taken as false. Where it stores the hit hole's colour into the shape (sticky for
+ * every later ray, render-order dependent) the hit record carries it instead: *hole = the hole
+ * whose body was hit, -1. */
+static int rpc_intersect(const Scene* s, const dt_shape_desc* sh, V3 ray, V3 start, float* t, int* inside,
+                         int* hole)
+{
+  float eps = 1e-4f;
+  float tmin, tmax;
+  *inside = 0;
+  if (!rpc_box(sh, ray, start, 0, &tmin, &tmax)) return 0;
+  if (tmax <= eps) return 0;
+  if (tmin < eps && tmax > eps) { *t = tmax; *inside = 1; }
+  *t = tmin;
+  float tcyl = FLT_MAX;
+  int inside_cyl = 0, hit = 0, cap_hit = 0, hit_cyl = -1;
+  for (int i = 0; i < sh->n_holes; i++) {
+    const dt_shape_desc* cyl = &s->d->holes[sh->hole_first + i];
+    float t_tmp = 0;
+    int inside_tmp = 0;
+    int hit_tmp = cyl_intersect(cyl, ray, start, &t_tmp, &inside_tmp);
+    if (hit_tmp) {
+      hit = 1;
+      if (t_tmp <= tcyl) { hit_cyl = i; inside_cyl = inside_tmp; tcyl = t_tmp; }
+    }
+    hit_tmp = cyl_intersect_cap(cyl, ray, start, &t_tmp, &inside_tmp);
+    if (hit_tmp) {
+      hit = 1;
+      if (t_tmp <= tcyl) { hit_cyl = i; cap_hit = 1; inside_cyl = inside_tmp; tcyl = t_tmp; }
+    }
+  }
+  if (hit) {
+    if (tcyl <= *t) {
+      if (cap_hit) return 0;
+      *inside = inside_cyl;
+      *t = tcyl;
+      *hole = hit_cyl;
+    }
+  }
+  return 1;
+}
+
+/* RectPrismWithCylinder::intersectShadow (1653-1790) */
+static int rpc_shadow(const Scene* s, const dt_shape_desc* sh, V3 ray, V3 start, float t_max)
+{
+  float eps = 1e-4f;
+  float tmin, tmax, t;
+  if (!rpc_box(sh, ray, start, 1, &tmin, &tmax)) return 0;
+  if (tmax <= eps) return 0;
+  if (tmin < eps && tmax > eps) {
+    if (tmax >= t_max) return 0;
+    t = tmax;
+  }
+  t = tmin;
+  float tcyl = FLT_MAX;
+  int hit = 0, cap_hit = 0;
+  for (int i = 0; i < sh->n_holes; i++) {
+    const dt_shape_desc* cyl = &s->d->holes[sh->hole_first + i];
+    float t_tmp = FLT_MIN;
+    int inside_tmp = 0;
+    int hit_tmp = cyl_intersect(cyl, ray, start, &t_tmp, &inside_tmp);
+    if (hit_tmp && t_tmp > eps && t_tmp < t_max) {
+      hit = 1;
+      if (t_tmp <= tcyl) tcyl = t_tmp;
+    }
+    hit_tmp = cyl_intersect_cap(cyl, ray, start, &t_tmp, &inside_tmp);
+    if (hit_tmp && t_tmp > eps && t_tmp < t_max) {
+      hit = 1;
+      if (t_tmp <= tcyl) { cap_hit = 1; tcyl = t_tmp; }
+    }
+  }
+  if (hit) {
+    if (tcyl <= t && tcyl > eps && tcyl < t_max) {
+      if (cap_hit) return 0;
+    }
+  }
+  return 1;
+}
+
+/* RectPrismWithCylinder::getNorm (1792-1821). lastHit is -1 whenever the shape is the closest hit
+ * (intersect resets it before `return true`). Past the three face tests the reference throws: counted
+ * as prism_norm_fallback; the hit hole's normal, else the front normal. */
+static V3 rpc_norm(const Ctx* c, const dt_shape_desc* sh, V3 point, int hole)
+{
+  float eps = 1e-3f;
+  V3 A = v3a(sh->v[0]), B = v3a(sh->v[1]), D = v3a(sh->v[3]), E = v3a(sh->v[4]);
+  V3 F = v3a(sh->v[5]), H = v3a(sh->v[7]);
+  V3 normbot = neg(normalized(cross(sub(F, E), sub(H, E))));
+  V3 normright = normalized(cross(sub(E, A), sub(D, A)));
+  V3 normfront = normalized(cross(sub(B, A), sub(E, A)));
+  if (dot(sub(point, A), normbot) <= eps) return normbot;
+  if (dot(sub(point, A), normright) <= eps) return normright;
+  if (dot(sub(point, A), normfront) <= eps) return normfront;
+  if (c->st) c->st->prism_norm_fallback++;
+  if (hole >= 0) return cyl_norm(&c->s->d->holes[sh->hole_first + hole], point);
+  return normfront;
+}
+
+/* RectPrism::getUV (1442-1461), inherited by RectPrismWithCylinder */
+static int rpc_uv(const dt_shape_desc* sh, V3 p, double* uo, double* vo)
+{
+  V3 A = v3a(sh->v[0]), C = v3a(sh->v[2]), D = v3a(sh->v[3]);
+  V3 ad = sub(D, A), dc = sub(C, D);
+  if (fabs(dot(cross(ad, dc), p)) <= 1e-5) {
+    float u = (float)(norm(cross(sub(p, A), ad)) / (norm(ad) * norm(dc)));
+    float v = (float)(norm(cross(sub(p, D), dc)) / (norm(dc) * norm(ad)));
+    *uo = u; *vo = v;
+    return 1;
+  }
+  *uo = -1; *vo = -1;
+  return 0;
+}
+
 /* GeoPrimitive::intersect dispatch. t is only written when the shape writes it (the
  * Checkerboard edge-on path returns true without setting t, Q16). hit_color receives the
  * colour the reference's intersect() would have stored into shape->color. */
 static int shape_intersect(const Ctx* c, int si, V3 ray, V3 start, float* t, int* inside,
-                           V3* hit_color)
+                           V3* hit_color, int* hole)
 {
   const dt_shape_desc* sh = SH(c->s, si);
   *hit_color = v3a(sh->color);
+  *hole = -1;
   switch (sh->type) {
+    case DT_SHAPE_RECTPRISM_CYL: {
+      int r = rpc_intersect(c->s, sh, ray, start, t, inside, hole);
+      if (r && *hole >= 0) *hit_color = v3a(c->s->d->holes[sh->hole_first + *hole].color);
+      return r;
+    }
     case DT_SHAPE_SPHERE:
       return sphere_intersect(v3a(sh->v[0]), sh->radius, ray, start, t, inside);
     case DT_SHAPE_CYLINDER:
@@ -666,6 +851,8 @@ static int shape_shadow(const Ctx* c, int si, V3 ray, V3 start, float t_max)
 {
   const dt_shape_desc* sh = SH(c->s, si);
   switch (sh->type) {
+    case DT_SHAPE_RECTPRISM_CYL:
+      return rpc_shadow(c->s, sh, ray, start, t_max);
     case DT_SHAPE_SPHERE:
       return sphere_shadow(v3a(sh->v[0]), sh->radius, ray, start, t_max);
     case DT_SHAPE_CYLINDER:
@@ -699,10 +886,11 @@ static int shape_shadow(const Ctx* c, int si, V3 ray, V3 start, float t_max)
 }
 
 /* GeoPrimitive::getNorm dispatch */
-static V3 shape_norm(const Ctx* c, int si, V3 p)
+static V3 shape_norm(const Ctx* c, int si, V3 p, int hole)
 {
   const dt_shape_desc* sh = SH(c->s, si);
   switch (sh->type) {
+    case DT_SHAPE_RECTPRISM_CYL: return rpc_norm(c, sh, p, hole);
     case DT_SHAPE_SPHERE: return sphere_norm(v3a(sh->v[0]), p);
     case DT_SHAPE_CYLINDER:
     case DT_SHAPE_CHECKER_CYLINDER: return cyl_norm(sh, p);
@@ -769,6 +957,7 @@ static int shape_uv(const Ctx* c, int si, V3 p, double* uo, double* vo)
 {
   const dt_shape_desc* sh = SH(c->s, si);
   switch (sh->type) {
+    case DT_SHAPE_RECTPRISM_CYL: return rpc_uv(sh, p, uo, vo);
     case DT_SHAPE_RECTANGLE: {
       float u, v;
       rect_uv(VX(c, sh, 0), VX(c, sh, 2), VX(c, sh, 3), p, &u, &v);
@@ -870,6 +1059,9 @@ static void shape_bounds(const dt_shape_desc* sh, V3* lb, V3* ub)
       *ub = cmax(v3(c1.x + r, c1.y + r, c1.z + r), v3(c2.x + r, c2.y + r, c2.z + r));
       return;
     }
+    case DT_SHAPE_RECTPRISM_CYL: /* RectPrism::getBounds (1382-1401) */
+      rpc_bounds(sh, lb, ub);
+      return;
     default: {
       int n = sh->type == DT_SHAPE_TRIANGLE ? 3 : (sh->type == DT_SHAPE_RECTPRISM_V2 ? 8 : 4);
       V3 mn = cmin(v3a(sh->v[0]), v3a(sh->v[1]));
@@ -1285,11 +1477,12 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
   float t_dist = FLT_MAX, t_min = FLT_MAX;
   int any_intersect = 0, inside = 0, hit_i = -1;
   V3 hit_shape_color = v3(0, 0, 0);
+  int hit_hole = -1;
   *in_motion = 0;
   for (int q = 0; q < n_inds; ++q) {
-    int ins = 0;
+    int ins = 0, hole = -1;
     V3 hc;
-    int r = shape_intersect(c, shape_inds[q], ray, eye, &t_dist, &ins, &hc);
+    int r = shape_intersect(c, shape_inds[q], ray, eye, &t_dist, &ins, &hc, &hole);
     if (r) {
       any_intersect = 1;
       *hit = 1;
@@ -1298,6 +1491,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
         inside = ins;  /* Q5: the reference reads an uninitialised variable here */
         t_min = t_dist;
         hit_shape_color = hc;
+        hit_hole = hole;
       }
     }
   }
@@ -1305,7 +1499,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
   const dt_shape_desc* hs = SH(s, hit_i);
 
   V3 isectP = add(eye, mul(t_min, ray));
-  V3 normal = shape_norm(c, hit_i, isectP);
+  V3 normal = shape_norm(c, hit_i, isectP, hit_hole);
   V3 in = normalized(ray);
   V3 shape_color = hit_shape_color;
   int model = hs->model;

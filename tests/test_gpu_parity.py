@@ -8,6 +8,8 @@ bounds only the FRACTION of channels outside 1e-4 (written next to it), leaving 
 1-ulp OCML-vs-glibc difference in an f64 transcendental that the reference's float quadratic
 solves can amplify at a silhouette.
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -483,3 +485,145 @@ def test_feature_scene_glass_spherelight_checkerboard(cuda):
 def _lib_stats():
     from distraytracer_amd import _lib
     return _lib.Stats()
+
+
+def _shape(shapes, t, **kw):
+    from distraytracer_amd import _lib
+    s = _lib.ShapeDesc()
+    s.type = t
+    s.tex_frame = -1
+    for k, v in kw.items():
+        if k == "v":
+            for i, p in enumerate(v):
+                for a in range(3):
+                    s.v[i][a] = p[a]
+        elif isinstance(v, (list, tuple)):
+            for a in range(len(v)):
+                getattr(s, k)[a] = v[a]
+        else:
+            setattr(s, k, v)
+    shapes.append(s)
+    return len(shapes) - 1
+
+
+def _rpc_scene():
+    """RectPrismWithCylinder (geometry.cpp:1467-1821) in every role the shipped prismcyl scene
+    never gives it: an axis-aligned wall with a hole (textured front face: RectPrism::getUV), a
+    tilted box with two holes (the box test uses the vertices' AABB), a steel mirror sphere inside
+    the first hole (its reflected rays start between the cap planes: the hole-body branch, boxes
+    entered from inside), a glass sphere, a floor, a back wall seen through the hole, a point light
+    behind the wall (shadow rays through the hole and past the light: the box test ignores t_max),
+    a point light in front and a rectangle light."""
+    import math
+    from distraytracer_amd import _lib
+    shapes, holes = [], []
+
+    def box(c, hx, hy, hz, rot):
+        """8 vertices A..H of a box rotated by `rot` about y: A B C D the x = -hx face, E..H = +x"""
+        cr, sr = math.cos(rot), math.sin(rot)
+        pts = [(-hx, -hy, -hz), (-hx, -hy, hz), (-hx, hy, hz), (-hx, hy, -hz)]
+        pts += [(hx, p[1], p[2]) for p in pts]
+        return [(c[0] + p[0] * cr + p[2] * sr, c[1] + p[1], c[2] - p[0] * sr + p[2] * cr) for p in pts]
+
+    def cyl(c1, c2, r, col):
+        h = _lib.ShapeDesc()
+        h.type, h.radius, h.tex_frame = 2, r, -1
+        for a in range(3):
+            h.v[0][a], h.v[1][a], h.color[a] = c1[a], c2[a], col[a]
+        holes.append(h)
+
+    wall = box((0.5, 0, 0), 0.5, 2, 2, 0.0)
+    _shape(shapes, 9, v=wall, color=(0.8, 0.2, 0.2), center=(0.5, 0, 0), hole_first=0, n_holes=1,
+           flags=4, tex_frame=0)
+    cyl((0, 0, 0), (1, 0, 0), 1.0, (0.2, 0.2, 0.9))
+    tilt = box((2.2, -1.2, 2.6), 0.4, 0.6, 0.7, 0.5)
+    _shape(shapes, 9, v=tilt, color=(0.2, 0.8, 0.3), center=(2.2, -1.2, 2.6), hole_first=1, n_holes=2)
+    cyl(tilt[0], tilt[4], 0.25, (0.9, 0.9, 0.1))
+    cyl(tilt[2], tilt[6], 0.2, (0.1, 0.9, 0.9))
+    _shape(shapes, 1, v=[(0.5, 0.1, -0.2)], radius=0.45, color=(0.9, 0.9, 0.9), material=2, center=(0.5, 0.1, -0.2))
+    _shape(shapes, 1, v=[(-1.6, -0.9, 1.4)], radius=0.5, color=(0.9, 0.9, 1.0), material=1, center=(-1.6, -0.9, 1.4))
+    _shape(shapes, 6, v=[(-8, -2.5, 6), (8, -2.5, 6), (8, -2.5, -6), (-8, -2.5, -6)], color=(0.5, 0.5, 0.5),
+           color1=(0.9, 0.9, 0.9), color2=(0.2, 0.2, 0.4), S=1.0, length=16.0, width=12.0, center=(0, -2.5, 0))
+    _shape(shapes, 4, v=[(6, -3, -6), (6, -3, 6), (6, 4, 6), (6, 4, -6)], color=(0.3, 0.6, 0.9), length=12.0,
+           width=7.0, center=(6, 0.5, 0))
+    ra, rb, rc, rd = (-2, 5, -1), (0, 5, -1), (0, 5, 1), (-2, 5, 1)
+    rl = _shape(shapes, 4, v=[ra, rb, rc, rd], color=(0.8, 0.8, 0.8), emit=2, flags=1, length=2.0, width=2.0,
+                center=(-1, 5, 0))
+    lights = (_lib.LightDesc * 3)()
+    for a in range(3):
+        lights[0].center[a] = (4.0, 0.2, 0.1)[a]
+        lights[0].color[a] = 0.9
+        lights[1].center[a] = (-4.0, 3.0, 3.0)[a]
+        lights[1].color[a] = 0.5
+        lights[2].center[a] = (-1, 5, 0)[a]
+        lights[2].color[a] = 0.7
+        lights[2].A[a], lights[2].B[a], lights[2].D[a] = ra[a], rb[a], rd[a]
+    lights[0].type, lights[0].shape_index = 1, -1
+    lights[1].type, lights[1].shape_index = 1, -1
+    lights[2].type, lights[2].shape_index = 3, rl
+    tex = bytes((i * 37 + 11) % 256 for i in range(8 * 8 * 3))
+    texbuf = (ctypes.c_uint8 * len(tex)).from_buffer_copy(tex)
+    textures = (_lib.TextureDesc * 1)()
+    textures[0].width, textures[0].height, textures[0].channels = 8, 8, 3
+    textures[0].pixels = ctypes.cast(texbuf, ctypes.POINTER(ctypes.c_uint8))
+    arr = (_lib.ShapeDesc * len(shapes))(*shapes)
+    harr = (_lib.ShapeDesc * len(holes))(*holes)
+    desc = _lib.SceneDesc(len(shapes), 3, 1, 0, arr, lights, textures, len(holes), 0, harr)
+    g = dt.globals_default()
+    g.use_model = 0
+    g.eye[0], g.eye[1], g.eye[2] = -5.0, 1.2, 2.8
+    g.lookingAt[0], g.lookingAt[1], g.lookingAt[2] = 0.6, -0.2, 0.3
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth, g.brdf_samples = 200, 150, 9, 5, 2
+    g.aperture, g.focal_length = 0.08, 6.0
+    return desc, g, (arr, harr, lights, textures, texbuf)
+
+
+def _render_desc(desc, g, frame=0):
+    h = ctypes.c_void_p()
+    dt.check(dt.lib.dt_scene_create(ctypes.byref(desc), ctypes.byref(g), ctypes.byref(h)), "dt_scene_create")
+    out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
+    st = _lib_stats()
+    dt.check(dt.lib.dt_render(h, ctypes.byref(g), frame, None, ctypes.c_void_p(out.data_ptr()), 1, None,
+                              ctypes.byref(st)), "dt_render")
+    dt.lib.dt_scene_destroy(h)
+    return out.cpu().numpy(), st
+
+
+def test_rectprism_cylinder_scene(cuda):
+    """RectPrismWithCylinder on the device (dt_trace_kernel_rpc) against the oracle: every hit,
+    shadow, normal and texel of the scene above, bit for bit, the same rays and shadow rays and
+    the same count of getNorm's off-prism points (the reference throws there)."""
+    desc, g, keep = _rpc_scene()
+    gpu, st = _render_desc(desc, g)
+    ref, rst = oracle.render(desc, g, 0, dt.tiles())
+    print("rpc scene: rays %d shadow %d prism_norm_fallback %d/%d uv %d tex %d" % (
+        st.rays, st.shadow_rays, st.prism_norm_fallback, rst.prism_norm_fallback, st.uv_out_of_range, st.tex_fetches))
+    # The wall's texture: RectPrism::getUV is valid only where |(ad x dc).p| <= 1e-5, elsewhere type 0
+    # aborts the shading (Q8) at the first unoccluded light. The device skips every shadow ray of
+    # such a point up front (it cannot change the colour), the oracle traces them as the reference
+    # does: fewer shadow rays on the device, never more.
+    assert st.rays == rst.rays and st.shadow_rays <= rst.shadow_rays
+    assert st.prism_norm_fallback == rst.prism_norm_fallback > 0   # hole-body hits (the mirror's rays)
+    assert st.rays > st.samples and st.nan_pixels == rst.nan_pixels
+    nan = np.isnan(ref)
+    assert np.array_equal(np.isnan(gpu), nan)
+    _cmp(np.where(nan, 0, gpu), np.where(nan, 0, ref), 0.001, "RectPrismWithCylinder scene")
+
+
+@pytest.mark.parametrize("frame,oblique", [(0, False), (7, False), (0, True)])
+def test_prismcyl_mode(cuda, frame, oblique):
+    """The reference's `./render prismcyl <n>` mode (render_final_project.cpp:1711-1723):
+    BuildScenePrismCylinder(n) at 640x480 with the globals' defaults (antialias 10 -> 9 spp,
+    depth 10, DoF); frame 0's camera looks straight down the hole's axis (a black frame, see
+    tests/test_host.py), so an oblique eye is rendered too."""
+    g = dt.globals_default()
+    built = dt.build_scene("prismcyl", frame, g)
+    g.xRes, g.yRes = 640, 480
+    if oblique:
+        g.eye[0], g.eye[1], g.eye[2] = -5.0, 1.3, 2.2
+    gpu, st = _render_gpu(built, g, frame, dt.tiles())
+    ref, rst = oracle.render(built, g, frame, dt.tiles())
+    assert st.rays == rst.rays and st.shadow_rays == rst.shadow_rays
+    _cmp(gpu, ref, 1e-4, "prismcyl frame %d%s" % (frame, " oblique" if oblique else ""))
+    if oblique:
+        assert ref.max() > 0

@@ -82,8 +82,49 @@ def test_build_final_tunnel_frames():
     assert g.focal_length == 20 and list(g.up) == [0, 0, -1]
 
 
+def test_build_prismcyl():
+    """BuildScenePrismCylinder (scene.h:3227-3263): one RectPrismWithCylinder (4x4x1 box at
+    x in [0, 1]) with one radius-1 cylinder hole along x through its centre, a point light; the
+    eye is rotated about itself, so it stays at og_eye up to rounding."""
+    g = dt.globals_default()
+    b = dt.build_scene("prismcyl", 7, g)
+    d = b.desc
+    assert d.n_shapes == 1 and d.n_lights == 1 and d.n_holes == 1
+    p = d.shapes[0]
+    assert SHAPE_TYPES[p.type] == "rectprism_cyl" and (p.hole_first, p.n_holes) == (0, 1)
+    assert [list(p.v[k]) for k in (0, 6)] == [[0, -2, -2], [1, 2, 2]]
+    assert list(p.color) == [1, 0, 0] and list(p.center) == [0.5, 0, 0]
+    h = d.holes[0]
+    assert SHAPE_TYPES[h.type] == "cylinder" and h.radius == 1
+    assert list(h.v[0]) == [0, 0, 0] and list(h.v[1]) == [1, 0, 0] and list(h.color) == [0, 0, 1]
+    assert list(g.eye) == pytest.approx([-6, 0.5, 1], abs=1e-12)
+    assert d.lights[0].type == 1 and list(d.lights[0].center) == [-5, 1, 0]
+
+
+def test_oracle_prismcyl_hole_and_face():
+    """RectPrismWithCylinder through the oracle (geometry.cpp:1507-1651). A camera ray toward the
+    box crosses the hole's front cap plane (x = 0) and enters the box there too; the two distances
+    are computed differently (-s.x / float(ray.x) against -s.x * (1 / ray.x)), and when the cap's is
+    not larger the ray passes (return false), even outside the hole's radius: intersectCap tests
+    planes. With the scene's own camera (eye (-6, 0.5, 1) looking along +x; the DoF offsets have no x
+    component) ray.x = 10 exactly, both distances round to 0.6f and every ray passes: the reference's
+    prismcyl frame 0 is black. From an oblique eye part of the rays stop on the red front face: red
+    speckle, never the hole's blue (its body branch needs the cap plane behind the ray's start)."""
+    g = dt.globals_default()
+    b = dt.build_scene("prismcyl", 0, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = 64, 48, 4, 2
+    img, st = oracle.render(b, g, 0, dt.tiles())
+    assert (img == 0).all() and st.rays == 64 * 48 * 4
+    g.eye[0], g.eye[1], g.eye[2] = -5.0, 1.3, 2.2
+    img, st = oracle.render(b, g, 0, dt.tiles())
+    px = img.reshape(48, 64, 3)
+    assert (px[..., 1] == 0).all() and (px[..., 2] == 0).all()
+    assert px[..., 0].max() > 0 and (px[..., 0] == 0).sum() > 0
+    assert st.prism_norm_fallback == 0      # every hit lies on the front face (getNorm's normbot)
+
+
 @pytest.mark.parametrize("name,frame,models", [("final", 240, 0), ("spheres", 0, 0), ("dof", 0, 0), ("hw4", 0, 0),
-                                               ("final", 0, 0), ("final", 480, 0), ("final", 2000, 0),
+                                               ("prismcyl", 3, 0), ("final", 0, 0), ("final", 480, 0), ("final", 2000, 0),
                                                ("final", 480, 1), ("final", 1200, 0), ("final", 1680, 0)])
 def test_bvh_topology_equals_oracle(name, frame, models):
     g = dt.globals_default()
