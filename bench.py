@@ -38,32 +38,71 @@ def build_globals(dt, cfg):
     return g, built
 
 
-def cpu_baseline(dt, cfg, frac_world):
-    """The CPU oracle (restatement of the reference loop, same RNG) on a bounded, spatially
-    uniform sample of the same frame: every `frac_world`-th 32x32 tile."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(dt, cfg, frac_world, scene, dev):
+    """The CPU oracle (the reference loop restated in C, same RNG) on a bounded, spatially uniform
+    sample of the same frame: rank 0's share of a `frac_world`-way tile split. SURVEY §8(d): the
+    host's cores (OpenMP dynamic), median of 3 after 1 warm-up, plus 1 core. The GPU renders the
+    same share into a slab beside it, and the two are compared (parity of the timed config), and the
+    oracle counts the include/dt_work.h events of the reference's loop on it."""
+    import statistics
+
     import numpy as np
+    import torch
 
     import oracle
     g, built = build_globals(dt, cfg)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    # the GPU box allots its CPU share through OMP_NUM_THREADS (16 per GPU there, while nproc shows the
+    # whole machine); elsewhere every core of the affinity mask
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(omp, affinity) if omp > 0 else affinity
     tile = dt.tiles(rank=0, world=frac_world, layout=dt.DT_OUT_SLAB)
-    out = np.zeros(dt.slab_floats(g, tile), dtype=np.float32)
-    t0 = time.perf_counter()
-    _, st = oracle.render(built, g, 240, tile, out=out, nthreads=threads)
-    dt_s = time.perf_counter() - t0
-    # single-core figure on a smaller slice (SURVEY 8d asks for both)
+    n = dt.slab_floats(g, tile)
+    out = np.zeros(n, dtype=np.float32)
+    _, st, work = oracle.render_work(built, g, 240, tile, out=out, nthreads=threads)   # warm-up (+ event counts)
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        _, st = oracle.render(built, g, 240, tile, out=out, nthreads=threads)
+        times.append(time.perf_counter() - t0)
+    dt_s = statistics.median(times)
+    # single core, on a 16x smaller share of the same split
     tile1 = dt.tiles(rank=0, world=frac_world * 16, layout=dt.DT_OUT_SLAB)
     out1 = np.zeros(dt.slab_floats(g, tile1), dtype=np.float32)
     t1 = time.perf_counter()
     _, st1 = oracle.render(built, g, 240, tile1, out=out1, nthreads=1)
     dt1 = time.perf_counter() - t1
-    return {"value": round(st.samples / dt_s / 1e6, 4), "unit": "Mpixel-samples/s", "cores": threads,
-            "kind": "port",
-            "sample": "oracle/oracle.c (OpenMP) on 1/%d of the frame's 32x32 tiles (rank 0's share of a %d-way "
-                      "tile split: %d pixels x %d spp), %.1f s wall" % (frac_world, frac_world, st.pixels,
-                                                                    st.samples // max(st.pixels, 1), dt_s),
-            "single_core": {"value": round(st1.samples / dt1 / 1e6, 4), "cores": 1,
-                            "sample": "1/%d of the tiles, %.1f s" % (frac_world * 16, dt1)}}
+    # parity of the timed config: the product path on the same share
+    gslab = torch.zeros(n, dtype=torch.float32, device=dev)
+    gst = dt.render(scene, g, 240, gslab, tile)
+    diff = np.abs(gslab.cpu().numpy().astype(np.float64) - out.astype(np.float64))
+    parity = {"pixels": int(st.pixels), "samples": int(st.samples), "max_abs": float(diff.max()),
+              "frac_gt_1e-4": float((diff > 1e-4).mean()),
+              "same_rays": bool(gst.rays == st.rays and gst.shadow_rays == st.shadow_rays),
+              "sample": "rank 0's share of a %d-way tile split of the timed frame, GPU slab vs oracle slab" % frac_world}
+    cpu = {"value": round(st.samples / dt_s / 1e6, 4), "unit": "Mpixel-samples/s", "cores": threads,
+           "kind": "port", "nproc": os.cpu_count(), "affinity_cpus": affinity, "omp_num_threads": omp or None,
+           "cpu_model": _cpu_model(),
+           "sample": "oracle/oracle.c (OpenMP, %d threads) on rank 0's share of a %d-way 32x32 tile split "
+                     "(%d pixels x %d spp), median of 3 runs after 1 warm-up: %s s"
+                     % (threads, frac_world, st.pixels, st.samples // max(st.pixels, 1),
+                        "/".join("%.2f" % t for t in times)),
+           "single_core": {"value": round(st1.samples / dt1 / 1e6, 4), "cores": 1,
+                           "sample": "rank 0's share of a %d-way split, %.1f s" % (frac_world * 16, dt1)}}
+    return cpu, parity, work, st.samples
 
 
 def end_to_end_ms(dt, cfg, dev):
@@ -78,6 +117,36 @@ def end_to_end_ms(dt, cfg, dev):
     t1 = time.perf_counter()
     scene.close()
     return round((t1 - t0) * 1e3, 3)
+
+
+def valu_roofline(cfg, kernel_ms, samples, ref_work=None, ref_samples=0):
+    """the binding roofline is the VALU. achieved = the include/dt_work.h events the
+    trace kernel executes for this frame (counted by the diagnostic library in a child process) x
+    their weights, / the trace kernel's HIP-event time; against the MI355X FP64 vector peak. The
+    reference loop's count for the same frame (the oracle's, scaled from its sample) beside it."""
+    from distraytracer_amd import work as W
+    dev = W.device_counts(cfg)
+    if dev is None:
+        return None
+    ops = dev["ops"] * (samples / max(dev["samples"], 1))   # the counting frame is the timed frame
+    achieved = ops / (kernel_ms / 1e3) / 1e12
+    r = {"bound": "valu", "achieved": round(achieved, 4), "peak": W.PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+         "frac": achieved / W.PEAK_FP64_TFLOPS,
+         "ops_per_launch": ops, "ops_per_sample": round(ops / samples, 2),
+         "kernel": "dt_trace_kernel", "kernel_ms": round(kernel_ms, 3),
+         "counts_per_sample": W.breakdown(dev["counts"], dev["samples"]),
+         "note": "FP64-equivalent VALU operations of the events the kernel executes (include/dt_work.h "
+                 "weights x libdt_work.so counts). Every operation is unfused (no FMA contraction, for "
+                 "parity), while the 78.6 TFLOP/s peak counts an FMA as 2: the ceiling for this code is "
+                 "half of it, frac_unfused_ceiling = 2 frac"}
+    r["frac_unfused_ceiling"] = round(2 * r["frac"], 5)
+    if ref_work is not None and ref_samples:
+        ref_ops = W.price(ref_work) / ref_samples
+        r["reference_loop"] = {"ops_per_sample": round(ref_ops, 2),
+                               "equivalent_tflops": round(ref_ops * samples / (kernel_ms / 1e3) / 1e12, 4),
+                               "note": "the reference's own loop (every leaf its boxes pass, the sky per "
+                                       "missing sample), counted by the oracle on the cpu_baseline sample"}
+    return r
 
 
 def load_pmc_traffic():
@@ -101,6 +170,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frac", type=int, default=8, help="CPU baseline renders 1/N of the tiles")
+    ap.add_argument("--no-roofline", action="store_true", help="skip the VALU work count (child process)")
     args = ap.parse_args()
 
     import torch
@@ -186,21 +256,37 @@ def main():
     if rank == 0:
         samples = W * H * spp * args.steps
         value = samples / elapsed / 1e6
-        # algorithmic bytes of one trace launch: framebuffer written once,
-        # texels read, scene read
-        flat_bytes = None
+        # HBM roofline, as north_star asks: algorithmic bytes of one trace launch =
+        # framebuffer written once, texels read, scene read
         px = lib_stats.pixels
         alg_bytes = px * 3 * 4 + lib_stats.tex_fetches * 3 + 70 * 1024
-        achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
-        peak = 8000.0
+        hbm_achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
         pmc = load_pmc_traffic() or {}
         if pmc.get("config", "c3") != args.config:
             pmc = {}   # the committed PMC profile is of another workload
         traffic = pmc.get("hbm_bytes_per_launch")
-        cpu = None
+        hbm = {"bound": "hbm", "achieved": round(hbm_achieved, 4), "peak": 8000.0, "unit": "GB/s",
+               "frac": hbm_achieved / 8000.0, "traffic": traffic,
+               "traffic_source": ("profiles/%s_summary.json (2*FETCH_SIZE + WRITE_SIZE, fabric requests "
+                                  "incl. Infinity-Cache hits: an upper bound on HBM bytes; mostly scratch)"
+                                  % pmc.get("tag")) if traffic else None,
+               "alg_bytes_per_launch": int(alg_bytes)}
+        cpu, parity, ref_work, ref_samples = None, None, None, 0
         e2e = end_to_end_ms(dt, args.config, dev) if world == 1 else None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(dt, args.config, args.cpu_frac)
+            cpu, parity, ref_work, ref_samples = cpu_baseline(dt, args.config, args.cpu_frac, scene, dev)
+        roof = None
+        if world == 1 and not args.no_roofline:
+            roof = valu_roofline(args.config, kernel_ms, W * H * spp, ref_work, ref_samples)
+        if roof is None:   # no diagnostic library (or N > 1): the HBM line alone
+            roof = dict(hbm, kernel="dt_trace_kernel", kernel_ms=round(kernel_ms, 3))
+        else:
+            roof["hbm"] = hbm
+        if pmc.get("valu_active_per_wave_cycle"):
+            roof["pmc"] = {"profile": "profiles/%s_summary.json" % pmc.get("tag"),
+                           "valu_active_per_wave_cycle": pmc.get("valu_active_per_wave_cycle"),
+                           "simd_busy": round(4 * pmc["valu_active_per_wave_cycle"], 3),
+                           "lane_utilisation": pmc.get("valu_lane_utilisation")}
         line = {
             "metric": "Mpixel-samples/s (W×H×spp/s) + wall-clock per frame, 1/2/4/8 GPU",
             "value": round(value, 3),
@@ -221,29 +307,14 @@ def main():
                        "name": args.config, "use_model": int(g.use_model),
                        "frame": 240, "xRes": W, "yRes": H, "spp": spp, "max_depth": g.max_depth,
                        "parallelism": "tile-split x%d + RCCL gather" % world if distributed else "single GPU"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 4), "peak": peak, "unit": "GB/s",
-                         "frac": achieved / peak, "traffic": traffic,
-                         "traffic_source": ("profiles/%s_summary.json (2*FETCH_SIZE + WRITE_SIZE, fabric requests "
-                                            "incl. Infinity-Cache hits: an upper bound on HBM bytes)" % pmc.get("tag"))
-                         if traffic else None,
-                         "valu": ({"active_per_wave_cycle": pmc.get("valu_active_per_wave_cycle"),
-                                   "simd_busy": round(4 * pmc["valu_active_per_wave_cycle"], 3),
-                                   "lane_utilisation": pmc.get("valu_lane_utilisation"),
-                                   "note": "binding unit (SURVEY 8d): VALU issue, 4 waves/SIMD; from the "
-                                           "committed PMC profile of this kernel"}
-                                  if pmc.get("valu_active_per_wave_cycle") else None),
-                         "kernel": "dt_trace_kernel", "kernel_ms": round(kernel_ms, 3),
-                         "alg_bytes_per_launch": int(alg_bytes),
-                         "note": "VALU-bound path (FP64 intersection/shading); HBM fraction reported as "
-                                 "north_star asks"},
+            "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity,
             "end_to_end_ms_per_frame": e2e,
             "work": {"rays_per_sample": round(lib_stats.rays / max(lib_stats.samples, 1), 3),
                      "shadow_rays_per_sample": round(lib_stats.shadow_rays / max(lib_stats.samples, 1), 3),
                      "stack_overflows": lib_stats.stack_overflows, "nan_pixels": lib_stats.nan_pixels},
         }
-        if flat_bytes:
-            line["scene_bytes"] = flat_bytes
         print(json.dumps(line), flush=True)
     scene.close()
     if distributed:

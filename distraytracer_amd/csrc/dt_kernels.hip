@@ -22,6 +22,7 @@
 #include <stdint.h>
 
 #include "../../include/dt.h"
+#include "../../include/dt_work.h"
 #include "dt_math.h"
 #include "dt_scene_dev.h"
 
@@ -43,12 +44,21 @@ using namespace dtd;
 #define DT_ACC(k, a, b)
 #endif
 
-// BVH work counters (box/prim tests, wave node visits) in dt_stats: compiled in only with
-// -DDT_WORK_COUNTERS (diagnostic builds): in the traversal loops they cost ~6% (C3)
+// Work counters (include/dt_work.h: the §8(d) event counts the VALU roofline prices): compiled in
+// only with -DDT_WORK_COUNTERS (the diagnostic library libdt_work.so; in the traversal loops they
+// cost several %). DT_WK(k, cond) adds the number of executing lanes with `cond` to event k: one
+// lane (the lowest such) adds the ballot's popcount to the wave's LDS counter, so the call sites may
+// sit in divergent code. Flushed to the stats block (dt_debug_counters) at kernel exit.
 #ifdef DT_WORK_COUNTERS
 #define DT_WORK(...) __VA_ARGS__
+#define DT_WK(k, cond)                                                                   \
+  do {                                                                                   \
+    const unsigned long long m_ = __ballot(cond);                                        \
+    if (m_ && (int)(threadIdx.x & 63) == (int)__builtin_ctzll(m_)) cnt.wk[(k)] += (unsigned)__popcll(m_); \
+  } while (0)
 #else
 #define DT_WORK(...)
+#define DT_WK(k, cond) do { } while (0)
 #endif
 
 // DT_WITH_RPC=1 (the second compilation of this file, build/dt_kernels_rpc.o): the trace kernel
@@ -1305,9 +1315,11 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
     tcull = (h.t_min == FLT_MAX || (DT_WITH_RPC && P.no_cull)) ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
 #endif
     bool hb = act & node_hit<GENERAL>(w, nd, shift, org, tcull);
-    DT_WORK(cnt.wnodes++; cnt.box += act);
+    DT_WORK(cnt.wnodes++);
+    DT_WK(DT_WK_BOX, act);
     DT_CNT(26);
     if (nd.meta & DN_LEAF) {
+      DT_WK(DT_WK_BOX, BUMP && hb);   // the exact bumped gather: the reference leaf's own box test
       if (BUMP && __ballot(hb)) hb = hb & bump_leaf_gathered(S, w, nd.skip, shift, org);
       if (__ballot(hb)) {
         DT_T(q0);
@@ -1319,7 +1331,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
           DT_CNT(8);
           DT_CNT(10 + (type & 7));   // closest-hit prim tests by type (8 -> 10)
           if (hb) {
-            DT_WORK(cnt.prim++);
+            DT_WK(DT_WK_HIT_SHAPE + type, true);
             int ins = 0, cc = -1;
             if (shape_hit(S, sid, type, flags, cas(S.geom) + off, ray, org, shift, t_dist, ins, cc, h.edge)) {
               any = true;
@@ -1377,8 +1389,10 @@ __device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams
     const DNodeDev nd = cas(BUMP ? S.bnodes : S.fnodes)[node];
     const float tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
     bool hb = active & node_hit<false>(w, nd, 0.0f, org, tcull);
+    DT_WK(DT_WK_BOX, active);
+    DT_WK(DT_WK_BOX, BUMP && hb);
     if (BUMP && __ballot(hb)) hb = hb & bump_leaf_gathered(S, w, nd.skip, shift, org);
-    DT_WORK(cnt.wnodes++; cnt.box += active);
+    DT_WORK(cnt.wnodes++);
     DT_CNT(26);
     if (__ballot(hb)) {
       const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
@@ -1390,7 +1404,7 @@ __device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams
         DT_CNT(8);
         DT_CNT(10 + (type & 7));
         if (hb) {
-          DT_WORK(cnt.prim++);
+          DT_WK(DT_WK_HIT_SHAPE + type, true);
           int ins = 0, cc = -1;
           if (shape_hit(S, sid, type, flags, cas(S.geom) + off2, ray, org, BUMP ? shift : 0.0f, t_dist, ins, cc, h.edge)) {
             any = true;
@@ -1456,7 +1470,7 @@ __device__ __forceinline__ void shadow_leaf(const DScene& S, const DNodeDev& nd,
     const unsigned long long occ_before = __ballot(occl);
 #endif
     if (test) {
-      DT_WORK(cnt.prim++);
+      DT_WK(DT_WK_SHADOW_SHAPE + type, true);
 #ifndef DT_ABL_NOPRIM_SHADOW
       if (shape_shadow(type, flags, cas(S.geom) + off, sn, sstart, t_max, shift)) occl = true;
 #endif
@@ -1511,12 +1525,14 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
     const DNodeDev nd = cas(NODES)[i];
     const bool act = GENERAL ? resume <= i : active & !occl;   // see closest_hit_walk
     bool hb = act & node_hit<GENERAL>(w, nd, shift, bstart, tcull);
-    DT_WORK(cnt.wnodes++; cnt.box += act);
+    DT_WORK(cnt.wnodes++);
+    DT_WK(DT_WK_BOX, act);
     DT_CNT(27);
 #ifdef DT_STAMPS
     ++nv;
 #endif
     if (nd.meta & DN_LEAF) {
+      DT_WK(DT_WK_BOX, BUMP && hb);
       if (BUMP && __ballot(hb)) hb = hb & bump_leaf_gathered(S, w, nd.skip, shift, bstart);
       if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, shift, cnt);
       if (GENERAL) {
@@ -1555,6 +1571,8 @@ __device__ bool occluded_list(const DScene& S, const Walk& w, bool active, V3 bs
     const DNodeDev nd = cas(S.nodes)[r];
     const bool hb = active & !occl &
                     (BUMP ? bump_leaf_gathered(S, w, r, shift, bstart) : node_hit<false>(w, nd, 0.0f, bstart, tcull));
+    DT_WK(DT_WK_BOX, active & !occl);
+    DT_WK(DT_WK_BOX, BUMP && active && !occl);
     DT_CNT(34);
     if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, shift, cnt);
     if (!__ballot(active & !occl)) break;
@@ -1597,6 +1615,8 @@ __device__ bool occluded_union(const DScene& S, const Walk& w, bool active, V3 b
     const DNodeDev nd = cas(S.nodes)[m];
     const bool hb = active & !occl &
                     (BUMP ? bump_leaf_gathered(S, w, m, shift, bstart) : node_hit<false>(w, nd, 0.0f, bstart, tcull));
+    DT_WK(DT_WK_BOX, active & !occl);
+    DT_WK(DT_WK_BOX, BUMP && active && !occl);
     DT_CNT(34);
     if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, shift, cnt);
     if (head == m) {
@@ -1748,6 +1768,9 @@ struct Counters {
   uint32_t rays, shadow, tex;        // per lane, wave-summed at exit
   uint32_t box, prim;
   uint32_t wnodes;                   // wave-level
+#ifdef DT_WORK_COUNTERS
+  unsigned int* wk;                  // the wave's DT_WK_N event counters (LDS)
+#endif
 #ifdef DT_STAMPS
   unsigned long long ph[64];   // diagnostic build only: cycles per phase, event counts (wave-uniform)
   int cur_li;                  // light of the current shadow test (per-shape histogram)
@@ -1971,6 +1994,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     bool shade = false;     // needs the light loop
     V3 own = v3(0, 0, 0);
     if (any) {
+      DT_WK(DT_WK_HIT, true);
       hd = S.hdr[sid];
       GP g = cas(S.geom) + hd.off;
       const DMat& M = S.mat[sid];
@@ -2009,6 +2033,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           } else {
             sp = base + nref;
             if (glass) {
+              DT_WK(DT_WK_REFRACT, true);
               float cos_theta = (float)dot(normal, neg(in));
               float sin_theta = (float)sqrt(1 - pw2((double)cos_theta));
               float r1 = h.inside ? P.refr_glass : P.refr_air, r2 = h.inside ? P.refr_air : P.refr_glass;
@@ -2033,6 +2058,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
               }
             }
             if (nref > 0 && glossy && !P.nogloss) {
+              DT_WK(DT_WK_GLOSSY_RECT, true);
               V3 A, B, C, D, wv, lv;
               glossy_rect(refl_ray, isectP, 2.0f, A, B, C, D, wv, lv);
               V3 wa = wv, la = lv;
@@ -2048,6 +2074,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
               // words 0-1 / 2-3 are their (x, y); gw keeps the odd attempt's words
               uint32_t gw[2] = {0u, 0u};
               for (int i = 0; i < nref; i++) {
+                DT_WK(DT_WK_GLOSSY, true);
                 int attempt = 0;
                 uint32_t o[4];
                 c.rng.draw_words(node, P_GLOSSY, (uint32_t)i << 8, o);
@@ -2057,6 +2084,8 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
                 bool exhausted = false;
                 while (dot(sample_refl, normal) <= 0) {
                   if (sample_limit < 0) { exhausted = true; break; }
+                  DT_WK(DT_WK_GLOSSY, true);
+                  DT_WK(DT_WK_GLOSSY_RECT, true);
                   float multiplier = (float)ldexp(1.0, 11 - sample_limit);   // pow(2, 11 - limit), exact
                   glossy_rect(refl_ray, isectP, multiplier, A, B, C, D, wv, lv);
                   attempt++;
@@ -2078,6 +2107,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
                 stack[base + nref - 1 - i] = ch;
               }
             } else if (nref > 0) {
+              DT_WK(DT_WK_MIRROR, true);
               Entry ch; ch.a = refl_ray; ch.b = add(isectP, mul(eps, refl_ray)); ch.k = k_refl * k;
               ch.depth = depth - 1; ch.key = child_key(node, 1); ch._pad = 0;
               stack[base] = ch;
@@ -2088,6 +2118,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
 
       // emissive (cpp:775-789)
       if (M.flags & DT_F_LIGHT) {
+        DT_WK(DT_WK_EMIT, true);
         if (M.emit == DT_EMIT_SPHERE) {
           float hitdot = (float)dot(in, normalized(sub(v3a(M.center), isectP)));
           double f = (0.1 * pw1((double)hitdot) + 0.05 * pw5((double)hitdot)) + 0.9;
@@ -2139,6 +2170,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
         float t_max = 0;
         V3 sn = v3(1, 0, 0);
         if (walk) {
+          DT_WK(DT_WK_LIGHT, true);
           // the first DT_LS_CACHE area lights park their sample pair in LDS for pass 2
           const int slot = li - DT_LS_FIRST;
           const bool cache = slot >= 0 && slot < DT_LS_CACHE;
@@ -2182,6 +2214,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
         const V3 e_dir = normalized(sub(eye2, isectP));
         const bool uv_oob = textured && (tu < 0 || tv < 0 || tu > 1 || tv > 1);
         if (vis != 0 && textured) {
+          DT_WK(DT_WK_TEX, true);
           const DMat& M = *Mp;
           if (uvt == 2) {
             shape_color = v3a(M.bordercolor);
@@ -2202,6 +2235,9 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           if (!(vis & (1u << li))) continue;
           const DT_CAS DLight& L = cas(S.lights)[li];
           const DMat& M = *Mp;
+#ifdef DT_WORK_COUNTERS
+          for (int m = 0; m < 4; ++m) DT_WK(DT_WK_BRDF + m, M.model == m);
+#endif
           const int slot = li - DT_LS_FIRST;
           const bool cache = slot >= 0 && slot < DT_LS_CACHE;
           const V3 sray = light_sample(c, L, li, isectP, node, nullptr, cache ? &lsxy[cache ? slot : 0][0][ln_] : nullptr,
@@ -2369,6 +2405,11 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   __shared__ unsigned long long item_s;
   Entry stack[DT_STACK_MAX];
   const int lane = threadIdx.x;
+#ifdef DT_WORK_COUNTERS
+  __shared__ unsigned int wk_lds[DT_WK_N];
+  if (lane < DT_WK_N) wk_lds[lane] = 0;
+  __syncthreads();
+#endif
   Ctx c;
   c.S = &S;
   c.P = &P;
@@ -2377,6 +2418,9 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   unsigned long long sky_px = 0;
   Counters cnt;
   cnt.rays = 0; cnt.shadow = 0; cnt.tex = 0; cnt.box = 0; cnt.prim = 0; cnt.wnodes = 0;
+#ifdef DT_WORK_COUNTERS
+  cnt.wk = wk_lds;
+#endif
 #ifdef DT_STAMPS
   for (int k = 0; k < 64; ++k) cnt.ph[k] = 0;
   cnt.cur_li = 0;
@@ -2444,6 +2488,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         // camera ray (cpp:1044-1072), regenerated per pass from the counter RNG (same values)
         // so that it is not held in registers across the DFS
         V3 eye_sample = v3a(P.eye), ray0 = v3(0, 0, 0);
+        DT_WK(DT_WK_CAMERA, act);
         if (act) camera_ray(c, P, px_x, px_y, eye_sample, ray0);
         PassOut po;
         ocol[0][lane] = 0; ocol[1][lane] = 0; ocol[2][lane] = 0;
@@ -2537,10 +2582,17 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   }
   {
     unsigned long long r = wave_sum(cnt.rays), sh = wave_sum(cnt.shadow), tx = wave_sum(cnt.tex);
-    unsigned long long bx = wave_sum(cnt.box), pr = wave_sum(cnt.prim);
+#ifdef DT_WORK_COUNTERS
+    __syncthreads();
+    if (lane < DT_WK_N && wk_lds[lane]) atomicAdd(S.stats + ST_N + 1 + lane, (unsigned long long)wk_lds[lane]);
     if (lane == 0) {
-      atomicAdd(S.stats + ST_BOX, bx);
+      unsigned long long pr = 0;
+      for (int k = DT_WK_HIT_SHAPE; k < DT_WK_HIT; ++k) pr += wk_lds[k];
+      atomicAdd(S.stats + ST_BOX, (unsigned long long)wk_lds[DT_WK_BOX]);
       atomicAdd(S.stats + ST_PRIM, pr);
+    }
+#endif
+    if (lane == 0) {
       atomicAdd(S.stats + ST_WNODES, (unsigned long long)cnt.wnodes);
 #ifdef DT_STAMPS
       for (int k = 0; k < 64; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);

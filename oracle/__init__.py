@@ -45,6 +45,9 @@ def oracle():
         o.or_render.restype = ctypes.c_int
         o.or_render.argtypes = [P(SceneDesc), P(Globals), ctypes.c_int, P(Tiles), ctypes.c_void_p, ctypes.c_int,
                                 P(Stats)]
+        o.or_render_work.restype = ctypes.c_int
+        o.or_render_work.argtypes = [P(SceneDesc), P(Globals), ctypes.c_int, P(Tiles), ctypes.c_void_p, ctypes.c_int,
+                                     P(Stats), P(ctypes.c_uint64)]
         o.or_sample_color.restype = ctypes.c_int
         o.or_sample_color.argtypes = [P(SceneDesc), P(Globals), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, P(ctypes.c_double), P(ctypes.c_int)]
@@ -80,6 +83,22 @@ def render(desc, g, frame, tile, out=None, nthreads=0):
     if rc:
         raise RuntimeError("or_render failed %d" % rc)
     return out, st
+
+
+def render_work(desc, g, frame, tile, out=None, nthreads=0):
+    """render(), also returning the include/dt_work.h event counts of the reference's loop
+    (numpy uint64[DT_WK_N])"""
+    from distraytracer_amd.work import N_EVENTS
+    if out is None:
+        out = np.zeros(3 * g.xRes * g.yRes, dtype=np.float32)
+    st = Stats()
+    work = np.zeros(N_EVENTS, dtype=np.uint64)
+    rc = oracle().or_render_work(_desc_ptr(desc), ctypes.byref(g), int(frame), ctypes.byref(tile),
+                                 ctypes.c_void_p(out.ctypes.data), int(nthreads), ctypes.byref(st),
+                                 work.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    if rc:
+        raise RuntimeError("or_render_work failed %d" % rc)
+    return out, st, work
 
 
 def render_sky(g, frame, tile, out=None, nthreads=0):

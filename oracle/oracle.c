@@ -20,6 +20,7 @@
  * pow(float,int) and pow(float,double) are double pow.
  */
 #include "oracle.h"
+#include "../include/dt_work.h"
 
 #include <float.h>
 #include <math.h>
@@ -320,7 +321,10 @@ typedef struct {
   Rng rng;
   float shift;     /* motion-blur y shift of "rectangle" shapes + leaf bump (cpp:1106-1160) */
   dt_stats* st;
+  uint64_t* wk;    /* include/dt_work.h event counts of the reference's loop (or_render_work), or NULL */
 } Ctx;
+
+#define WK(c, k) do { if ((c)->wk) (c)->wk[(k)]++; } while (0)
 
 static inline const dt_shape_desc* SH(const Scene* s, int i) { return &s->d->shapes[i]; }
 
@@ -787,6 +791,7 @@ static int shape_intersect(const Ctx* c, int si, V3 ray, V3 start, float* t, int
   const dt_shape_desc* sh = SH(c->s, si);
   *hit_color = v3a(sh->color);
   *hole = -1;
+  if (sh->type > 0 && sh->type < 10) WK(c, DT_WK_HIT_SHAPE + sh->type);
   switch (sh->type) {
     case DT_SHAPE_RECTPRISM_CYL: {
       int r = rpc_intersect(c->s, sh, ray, start, t, inside, hole);
@@ -850,6 +855,7 @@ static int shape_intersect(const Ctx* c, int si, V3 ray, V3 start, float* t, int
 static int shape_shadow(const Ctx* c, int si, V3 ray, V3 start, float t_max)
 {
   const dt_shape_desc* sh = SH(c->s, si);
+  if (sh->type > 0 && sh->type < 10) WK(c, DT_WK_SHADOW_SHAPE + sh->type);
   switch (sh->type) {
     case DT_SHAPE_RECTPRISM_CYL:
       return rpc_shadow(c->s, sh, ray, start, t_max);
@@ -1340,6 +1346,7 @@ static int bvh_gather(const Ctx* c, V3 ray, V3 start, int* out)
   V3 inv_ray = v3(1.0 / ray.x, 1.0 / ray.y, 1.0 / ray.z);
   while (sp > 0) {
     const BNode* b = &s->nodes[stack[--sp]];
+    WK(c, DT_WK_BOX);
     if (box_intersect(b, c->shift, ray, inv_ray, start)) {
       if (b->leaf && b->count > 0) {
         for (int i = 0; i < b->count; ++i) out[n++] = s->idx[b->first + i];
@@ -1497,6 +1504,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
   }
   if (!any_intersect || hit_i < 0) { free(shape_inds); return; }
   const dt_shape_desc* hs = SH(s, hit_i);
+  WK(c, DT_WK_HIT);
 
   V3 isectP = add(eye, mul(t_min, ray));
   V3 normal = shape_norm(c, hit_i, isectP, hit_hole);
@@ -1515,6 +1523,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
     int glossy = (hs->flags & DT_F_GLOSSY) != 0;
     float k_refl = 1, k_refr = 1;
     if (material == DT_MAT_GLASS) {
+      WK(c, DT_WK_REFRACT);
       float cos_theta = (float)dot(normal, neg(in));
       float sin_theta = (float)sqrt(1 - pow(cos_theta, 2));
       V3 out;
@@ -1534,6 +1543,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
     } else if (dot(refl_ray, normal) > eps) {
       if (glossy && !g->nogloss) {
         V3 A, B, C, D, wv, lv;
+        WK(c, DT_WK_GLOSSY_RECT);
         glossy_rect(refl_ray, isectP, 2.0f, &A, &B, &C, &D, &wv, &lv);
         V3 width_adj = wv;
         if (dot(wv, normal) <= 0) width_adj = neg(width_adj);
@@ -1547,6 +1557,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
           int hit_tmp = 0;
           int attempt = 0;
           double u0, u1;
+          WK(c, DT_WK_GLOSSY);
           glossy_xy(&c->rng, node, i, attempt, &u0, &u1);
           V3 sample_refl = sub(rect_sample(A, B, D, u0, u1), isectP);
           int sample_limit = 10;
@@ -1554,6 +1565,8 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
           while (dot(sample_refl, normal) <= 0) {
             if (sample_limit < 0) { exhausted = 1; break; }
             float multiplier = (float)pow(2, 11 - sample_limit);
+            WK(c, DT_WK_GLOSSY);
+            WK(c, DT_WK_GLOSSY_RECT);
             glossy_rect(refl_ray, isectP, multiplier, &A, &B, &C, &D, &wv, &lv);
             attempt++;
             glossy_xy(&c->rng, node, i, attempt, &u0, &u1);
@@ -1568,6 +1581,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
                     in_motion, k_refl * k / g->brdf_samples, child_key(node, 2 + i));
         }
       } else {
+        WK(c, DT_WK_MIRROR);
         ray_color(c, refl_ray, add(isectP, mul(eps, refl_ray)), depth - 1, color, hit, in_motion,
                   k_refl * k, child_key(node, 1));
       }
@@ -1576,6 +1590,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
 
   /* SHADING (771-960) */
   if (hit_light) {
+    WK(c, DT_WK_EMIT);
     if (hs->emit == DT_EMIT_SPHERE) {
       float hitdot = (float)dot(in, normalized(sub(v3a(hs->center), isectP)));
       double f = (0.1 * pow(hitdot, 1) + 0.05 * pow(hitdot, 5)) + 0.9;
@@ -1595,6 +1610,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
     V3 tmp_color = v3(0, 0, 0);
     for (int li = 0; li < s->d->n_lights; ++li) {
       const dt_light_desc* L = &s->d->lights[li];
+      WK(c, DT_WK_LIGHT);
       V3 sray = light_sample(c, li, isectP, node);
       float t_max = (float)norm(sray);
       int shadow = 1;
@@ -1614,6 +1630,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
       V3 lc = v3a(L->color);
       if (hs->flags & DT_F_TEXTURE) {
         double u, v;
+        WK(c, DT_WK_TEX);
         int type = shape_uv(c, hit_i, isectP, &u, &v);
         if (type == 0) { free(shape_inds); return; }   /* Q8 */
         if (u < 0 || v < 0 || u > 1 || v > 1) {
@@ -1633,6 +1650,7 @@ static void ray_color(const Ctx* c, V3 ray, V3 eye, int depth, V3* color, int* h
           shape_color = v3(px[0] / 255.0, px[1] / 255.0, px[2] / 255.0);
         }
       }
+      if (model >= 0 && model < 4) WK(c, DT_WK_BRDF + model);
       if (model == DT_MODEL_OREN_NAYAR) {  /* 894-913 */
         float A = (float)(1.0 - (0.5 * pow(roughness, 2)) / (pow(roughness, 2) + 0.33));
         float B = (float)((0.45 * pow(roughness, 2)) / (pow(roughness, 2) + 0.09));
@@ -1848,12 +1866,14 @@ static int render_setup(RenderCtx* R, const dt_scene_desc* d, const dt_globals* 
 
 /* one sample of renderImage's inner loop (cpp:1062-1211) */
 static void render_sample(const RenderCtx* R, const dt_globals* g, int x, int y, int i, V3* out,
-                          int* out_hit, dt_stats* st)
+                          int* out_hit, dt_stats* st, uint64_t* wk)
 {
   const Cam* cam = &R->cam;
   Ctx c;
   c.s = &R->scene;
   c.st = st;
+  c.wk = wk;
+  WK(&c, DT_WK_CAMERA);
   c.shift = 0.0f;
   c.rng.key[0] = g->seed;
   c.rng.key[1] = (uint32_t)R->frame;
@@ -1881,6 +1901,7 @@ static void render_sample(const RenderCtx* R, const dt_globals* g, int x, int y,
       or_cloud_color(g, pr, o, (float)R->frame, col);
       tmp_color = v3a(col);
       if (st) st->sky_pixels++;
+      WK(&c, DT_WK_SKY);
     } else {
       tmp_color = v3a(g->default_col);
     }
@@ -1900,6 +1921,7 @@ static void render_sample(const RenderCtx* R, const dt_globals* g, int x, int y,
       }
       Ctx cm = c;
       cm.shift = val;
+      WK(&c, DT_WK_CAMERA);
       V3 motion_color = v3(0, 0, 0);
       ray_color(&cm, sub(focalPoint, eye_sample), eye_sample, g->max_depth, &motion_color, &hit, &motion,
                 1.0f, root_key(m + 1));
@@ -1909,6 +1931,7 @@ static void render_sample(const RenderCtx* R, const dt_globals* g, int x, int y,
           double pr[3] = {point.x, point.y, point.z}, o[3] = {0, 0, 0}, col[3];
           or_cloud_color(g, pr, o, (float)R->frame, col);
           motion_color = v3a(col);
+          WK(&c, DT_WK_SKY);
         } else {
           motion_color = v3a(g->default_col);
         }
@@ -1928,15 +1951,25 @@ int or_sample_color(const dt_scene_desc* d, const dt_globals* g, int frame, int 
   int rc = render_setup(&R, d, g, frame);
   if (rc == DT_OK) {
     V3 col;
-    render_sample(&R, g, x, y, sample, &col, out_hit, NULL);
+    render_sample(&R, g, x, y, sample, &col, out_hit, NULL, NULL);
     out_color[0] = col.x; out_color[1] = col.y; out_color[2] = col.z;
   }
   scene_free(&R.scene);
   return rc;
 }
 
+int or_render_work(const dt_scene_desc* d, const dt_globals* g, int frame, const dt_tiles* tiles, float* out,
+                   int nthreads, dt_stats* stats, uint64_t* work);
+
 int or_render(const dt_scene_desc* d, const dt_globals* g, int frame, const dt_tiles* tiles, float* out,
               int nthreads, dt_stats* stats)
+{
+  return or_render_work(d, g, frame, tiles, out, nthreads, stats, NULL);
+}
+
+/* or_render, also counting the include/dt_work.h events of the reference's loop into work[DT_WK_N] */
+int or_render_work(const dt_scene_desc* d, const dt_globals* g, int frame, const dt_tiles* tiles, float* out,
+                   int nthreads, dt_stats* stats, uint64_t* work)
 {
   RenderCtx R;
   int rc = render_setup(&R, d, g, frame);
@@ -1953,6 +1986,8 @@ int or_render(const dt_scene_desc* d, const dt_globals* g, int frame, const dt_t
   {
     dt_stats local;
     memset(&local, 0, sizeof(local));
+    uint64_t wk[DT_WK_N];
+    memset(wk, 0, sizeof(wk));
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic, 4)
 #endif
@@ -1963,7 +1998,7 @@ int or_render(const dt_scene_desc* d, const dt_globals* g, int frame, const dt_t
       V3 color = v3(0, 0, 0);
       for (int i = 0; i < R.sampled_n; i++) {
         V3 tc;
-        render_sample(&R, g, x, y, i, &tc, NULL, &local);
+        render_sample(&R, g, x, y, i, &tc, NULL, &local, work ? wk : NULL);
         color = add(color, tc);
       }
       color = divs(color, R.sampled_n);
@@ -1984,6 +2019,8 @@ int or_render(const dt_scene_desc* d, const dt_globals* g, int frame, const dt_t
       total.spherelight_exhausted += local.spherelight_exhausted;
       total.prism_norm_fallback += local.prism_norm_fallback;
       total.reflect_errors += local.reflect_errors; total.nan_pixels += local.nan_pixels;
+      if (work)
+        for (int k = 0; k < DT_WK_N; ++k) work[k] += wk[k];
     }
   }
   if (stats) *stats = total;

@@ -55,6 +55,12 @@ int or_bvh(const dt_scene_desc* d, const dt_globals* g, dt_bvh_node* nodes, int 
 int or_render(const dt_scene_desc* d, const dt_globals* g, int frame, const dt_tiles* tiles,
               float* out, int nthreads, dt_stats* stats);
 
+/* or_render, also adding the include/dt_work.h event counts of the reference's loop (every box
+ * its gathers test, every intersect / intersectShadow call, light, BRDF, texel, sky march) into
+ * work[DT_WK_N] (zeroed by the caller) */
+int or_render_work(const dt_scene_desc* d, const dt_globals* g, int frame, const dt_tiles* tiles,
+                   float* out, int nthreads, dt_stats* stats, uint64_t* work);
+
 /* one rayColor call tree for a single pixel-sample (debug / unit tests) */
 int or_sample_color(const dt_scene_desc* d, const dt_globals* g, int frame, int x, int y,
                     int sample, double out_color[3], int* out_hit);
