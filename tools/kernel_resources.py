@@ -41,11 +41,17 @@ def resources(obj):
 
 
 if __name__ == "__main__":
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    obj = args[0] if args else os.path.join(os.path.dirname(__file__), "..", "distraytracer_amd", "csrc", "build",
-                                            "dt_kernels.o")
-    r = resources(obj)
+    import argparse
+    ap = argparse.ArgumentParser()
+    build = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "distraytracer_amd", "csrc", "build")
+    ap.add_argument("objects", nargs="*", default=[os.path.join(build, "dt_kernels.o"),
+                                                   os.path.join(build, "dt_kernels_rpc.o")])
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    r = {}
+    for obj in a.objects:
+        r.update(resources(obj))
     print(json.dumps(r, indent=1))
-    if "--json" in sys.argv:
-        with open(sys.argv[sys.argv.index("--json") + 1], "w") as f:
+    if a.json:
+        with open(a.json, "w") as f:
             json.dump(r, f, indent=1)
