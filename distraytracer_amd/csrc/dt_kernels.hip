@@ -113,6 +113,9 @@ using namespace dtd;
 #ifndef DT_LS_CACHE
 #define DT_LS_CACHE 4   // lights whose area-sample pair is kept in LDS between the two light passes
 #endif
+#ifndef DT_LAZY_ENTRY
+#define DT_LAZY_ENTRY 1   // the popped DFS entry's fields re-read from its stack slot where used (run_pass)
+#endif
 
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
        ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15, ST_N = 16 };
@@ -1764,8 +1767,18 @@ struct PassOut {
 
 // per-lane event counters, kept in registers for the whole persistent loop and reduced
 // across the wave once at kernel exit (same-address atomics per lane serialise at L2)
+// wave-level event counters of dt_stats (rays, shadow rays, texel fetches) in the wave's LDS: one
+// lane adds the ballot's popcount. Per-lane counters in VGPRs were live across every walk and
+// spilled/reloaded around them (a scratch store per light iteration).
+enum { WC_RAYS = 0, WC_SHADOW = 1, WC_TEX = 2, WC_N = 3 };
+#define DT_WCNT(k, cond)                                                                 \
+  do {                                                                                   \
+    const unsigned long long m_ = __ballot(cond);                                        \
+    if (m_ && (int)(threadIdx.x & 63) == (int)__builtin_ctzll(m_)) cnt.wc[(k)] += (unsigned)__popcll(m_); \
+  } while (0)
+
 struct Counters {
-  uint32_t rays, shadow, tex;        // per lane, wave-summed at exit
+  unsigned int* wc;                  // WC_N wave counters (LDS), flushed at exit
   uint32_t box, prim;
   uint32_t wnodes;                   // wave-level
 #ifdef DT_WORK_COUNTERS
@@ -1914,6 +1927,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     // pop FINISH entries (own-light contributions), then the next NODE
     bool have = false;
     Entry e;
+    int pidx = 0;   // DT_LAZY_ENTRY: the popped NODE entry's slot
     while (sp > 0) {
 #if DT_FIN_PARTIAL
       // read the depth word first: a FINISH entry only carries its colour
@@ -1925,7 +1939,11 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
         ocol[1][l] = ocol[1][l] + a.y;
         ocol[2][l] = ocol[2][l] + a.z;
       } else if (d > 0) {
+#if DT_LAZY_ENTRY
+        pidx = sp;
+#else
         e = stack[sp];
+#endif
         have = true;
         break;
       }
@@ -1953,12 +1971,23 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     // the host enables it for tile splits only (P.prio_steps).
     if (++prio_steps == P.prio_steps) __builtin_amdgcn_s_setprio(DT_PRIO_LEVEL);
 #endif
-    const V3 ray = e.a, eye = e.b;
+#if DT_LAZY_ENTRY
+    // The popped NODE entry stays in its stack slot until this step's FINISH record overwrites it
+    // at the very end (the FINISH slot is that same slot), so its fields are read from there where
+    // they are used, behind compiler barriers, instead of being held in registers across the walks:
+    // the allocator spilled them to scratch right after the pop, a store of data already there.
+#define DT_EF(f) (stack[pidx].f)
+    V3 ray = DT_EF(a), eye = DT_EF(b);
+    const bool is_root = have && DT_EF(_pad) == 1;
+#else
+    V3 ray = e.a, eye = e.b;
     const int depth = e.depth;
     const float k = e.k;
     const uint32_t node = e.key;
     const bool is_root = have && e._pad == 1;
-    if (have) { out.in_motion = false; cnt.rays++; }   // cpp:519
+#endif
+    if (have) out.in_motion = false;   // cpp:519
+    DT_WCNT(WC_RAYS, have);
 
     DT_T(t1);
     DT_ACC(0, t0, t1);
@@ -1977,6 +2006,14 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       if (!__ballot(have && blk != b0)) pblock = b0;
     }
     bool any = closest_hit(S, P, have, ray, eye, shift, h, cnt, pblock);
+#if DT_LAZY_ENTRY
+    asm volatile("" ::: "memory");   // the entry's fields: fresh loads, not values kept across the walk
+    ray = DT_EF(a);
+    eye = DT_EF(b);
+    const int depth = DT_EF(depth);
+    const float k = DT_EF(k);
+    const uint32_t node = DT_EF(key);
+#endif
 #ifdef DT_STAMPS
     if (__ballot(is_root)) { cnt.ph[46] += cnt.ph[26] - v_before; cnt.ph[39] += 1; }
 #endif
@@ -2178,7 +2215,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
                               cache ? 1 : 0, pair);
           t_max = (float)norm(sray);
           sn = normalized(sray);
-          cnt.shadow++;
+          DT_WCNT(WC_SHADOW, true);
         }
         DT_T(t4);
 #ifdef DT_STAMPS
@@ -2247,7 +2284,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           V3 lc = v3a(L.color);
           if (textured) {
             if (uv_oob) atomicAdd(S.stats + ST_UV, 1ull);   // the reference terminates here (Q9)
-            if (uvt == 1 && M.tex >= 0) cnt.tex++;
+            DT_WCNT(WC_TEX, uvt == 1 && M.tex >= 0);
           }
           V3 ray_col;
           const float roughness = M.roughness;
@@ -2417,7 +2454,11 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   c.rng.k1 = (uint32_t)P.frame;
   unsigned long long sky_px = 0;
   Counters cnt;
-  cnt.rays = 0; cnt.shadow = 0; cnt.tex = 0; cnt.box = 0; cnt.prim = 0; cnt.wnodes = 0;
+  __shared__ unsigned int wc_lds[WC_N];
+  if (lane < WC_N) wc_lds[lane] = 0;
+  __syncthreads();
+  cnt.wc = wc_lds;
+  cnt.box = 0; cnt.prim = 0; cnt.wnodes = 0;
 #ifdef DT_WORK_COUNTERS
   cnt.wk = wk_lds;
 #endif
@@ -2581,7 +2622,8 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     ++item;
   }
   {
-    unsigned long long r = wave_sum(cnt.rays), sh = wave_sum(cnt.shadow), tx = wave_sum(cnt.tex);
+    __syncthreads();
+    const unsigned long long r = wc_lds[WC_RAYS], sh = wc_lds[WC_SHADOW], tx = wc_lds[WC_TEX];
 #ifdef DT_WORK_COUNTERS
     __syncthreads();
     if (lane < DT_WK_N && wk_lds[lane]) atomicAdd(S.stats + ST_N + 1 + lane, (unsigned long long)wk_lds[lane]);

@@ -70,3 +70,41 @@ class GatherPipeline:
         work.wait()   # orders torch's current stream after the collective
         if self.split.rank == 0:
             self.split.assemble(self.gathered[b], self.image)   # on that same stream
+
+
+class FrameQueue:
+    """Frame-parallel animation (C5): frames handed out one at a time from a shared
+    counter in the process group's store, in descending order of their estimated cost (longest
+    processing time first: the room-to-tunnel transition frames, up to ~50x the mean, go out first
+    and the cheap ones fill the tails). A rank asks for its next frame when it starts preparing it,
+    so a rank that drew an expensive frame simply takes fewer. No collective on the data path: the
+    store counter is a host-side atomic add.
+
+    frames: the frame ids to render; cost: {frame id: estimated cost} (missing ids: the mean);
+    store: a torch.distributed Store (None: a single process, plain iteration)."""
+
+    def __init__(self, frames, cost=None, store=None, key="dt_frame_queue"):
+        cost = cost or {}
+        known = [cost[n] for n in frames if n in cost]
+        mean = sum(known) / len(known) if known else 1.0
+        # stable: equal costs keep the frames' own order
+        self.order = sorted(frames, key=lambda n: -cost.get(n, mean))
+        self.store = store
+        self.key = key
+        self._local = 0
+
+    def next(self):
+        """the next frame id, or None when every frame has been handed out"""
+        if self.store is None:
+            i = self._local
+            self._local += 1
+        else:
+            i = int(self.store.add(self.key, 1)) - 1
+        return self.order[i] if i < len(self.order) else None
+
+    def __iter__(self):
+        while True:
+            n = self.next()
+            if n is None:
+                return
+            yield n

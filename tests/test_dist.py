@@ -112,3 +112,48 @@ def test_tile_split_gather_equals_single_rank(tmp_path, world, cfg):
     g, b = _scene(cfg)
     ref, _ = oracle.render(b, g, 240, dt.tiles(), nthreads=4)
     assert np.array_equal(got, ref)   # bit-identical for any world size
+
+
+def _queue_worker(rank, world, port, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import time
+        from distraytracer_amd.multigpu import FrameQueue
+        frames = list(range(0, 40, 2))
+        cost = {n: float(n % 7 + (50 if n == 24 else 0)) for n in frames}
+        q = FrameQueue(frames, cost, dist.distributed_c10d._get_default_store())
+        got = []
+        for n in q:
+            got.append(n)
+            time.sleep(0.002 * cost[n])   # "render": a rank holding a costly frame takes fewer
+        everyone = [None] * world
+        dist.all_gather_object(everyone, got)
+        if rank == 0:
+            with open(result_path, "w") as f:
+                import json
+                json.dump({"per_rank": everyone, "order": q.order}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_frame_queue_hands_out_every_frame_once(tmp_path):
+    """C5 frame-parallel (tools/animate.py --split frames): the store counter hands every frame to
+    exactly one rank, most expensive first (LPT); each rank sees its frames in queue order."""
+    import json
+    out = str(tmp_path / "q.json")
+    mp.start_processes(_queue_worker, args=(3, _free_port(), out), nprocs=3, join=True, start_method="spawn")
+    r = json.load(open(out))
+    flat = sorted(n for lst in r["per_rank"] for n in lst)
+    assert flat == list(range(0, 40, 2))
+    order = r["order"]
+    assert order[0] == 24                      # the costliest frame goes out first
+    for lst in r["per_rank"]:
+        pos = [order.index(n) for n in lst]
+        assert pos == sorted(pos)
+
+
+def test_frame_queue_single_process():
+    from distraytracer_amd.multigpu import FrameQueue
+    q = FrameQueue([5, 1, 3, 9], {5: 1.0, 1: 10.0, 9: 10.0})   # 3 unknown: the mean (7)
+    assert list(q) == [1, 9, 3, 5]
