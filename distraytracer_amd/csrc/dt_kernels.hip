@@ -113,6 +113,12 @@ using namespace dtd;
 #ifndef DT_LS_CACHE
 #define DT_LS_CACHE 4   // lights whose area-sample pair is kept in LDS between the two light passes
 #endif
+#ifndef DT_FIN_LEAF
+#define DT_FIN_LEAF 1     // a node without children adds its own light at once instead of through a FINISH entry
+#endif
+#ifndef DT_LAZY_LIGHT
+#define DT_LAZY_LIGHT 0   // 1: its node key / k re-read inside the light loops (volatile loads): C3 -2.7% (r03f)
+#endif
 #ifndef DT_LAZY_ENTRY
 #define DT_LAZY_ENTRY 1   // the popped DFS entry's fields re-read from its stack slot where used (run_pass)
 #endif
@@ -1977,6 +1983,15 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     // they are used, behind compiler barriers, instead of being held in registers across the walks:
     // the allocator spilled them to scratch right after the pop, a store of data already there.
 #define DT_EF(f) (stack[pidx].f)
+#if DT_LAZY_LIGHT
+    // node key and k of the entry, re-read (volatile: never replaced by a value held in a register)
+    // inside the light loops, whose every iteration holds a shadow walk
+#define DT_EF_NODE (*(volatile const uint32_t*)&stack[pidx].key)
+#define DT_EF_K (*(volatile const float*)&stack[pidx].k)
+#else
+#define DT_EF_NODE node
+#define DT_EF_K k
+#endif
     V3 ray = DT_EF(a), eye = DT_EF(b);
     const bool is_root = have && DT_EF(_pad) == 1;
 #else
@@ -2211,7 +2226,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           // the first DT_LS_CACHE area lights park their sample pair in LDS for pass 2
           const int slot = li - DT_LS_FIRST;
           const bool cache = slot >= 0 && slot < DT_LS_CACHE;
-          sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL, cache ? &lsxy[cache ? slot : 0][0][ln_] : nullptr,
+          sray = light_sample(c, L, li, isectP, DT_EF_NODE, S.stats + ST_SPHL, cache ? &lsxy[cache ? slot : 0][0][ln_] : nullptr,
                               cache ? 1 : 0, pair);
           t_max = (float)norm(sray);
           sn = normalized(sray);
@@ -2277,7 +2292,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
 #endif
           const int slot = li - DT_LS_FIRST;
           const bool cache = slot >= 0 && slot < DT_LS_CACHE;
-          const V3 sray = light_sample(c, L, li, isectP, node, nullptr, cache ? &lsxy[cache ? slot : 0][0][ln_] : nullptr,
+          const V3 sray = light_sample(c, L, li, isectP, DT_EF_NODE, nullptr, cache ? &lsxy[cache ? slot : 0][0][ln_] : nullptr,
                                        cache ? 2 : 0);
           const V3 sn = normalized(sray);
           const V3 normal = nrm;
@@ -2344,7 +2359,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
           }
           if (!is_approx_zero(ray_col)) {
             hits++;
-            tmp_color = add(tmp_color, mul(k, ray_col));
+            tmp_color = add(tmp_color, mul(DT_EF_K, ray_col));
           }
         }
         if (hits > 0) own = divs(tmp_color, hits);
@@ -2353,6 +2368,18 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
     DT_T(t6);
     DT_ACC(4, t3, t6);
     if (fin_slot >= 0) {
+#if DT_FIN_LEAF
+      if (sp == fin_slot + 1) {
+        // no children were pushed: the FINISH entry would be the very next pop, so the own light
+        // goes into the accumulator now, in the same order, without a stack round trip
+        sp = fin_slot;
+        const int l = threadIdx.x & (DT_WAVE - 1);
+        ocol[0][l] = ocol[0][l] + own.x;
+        ocol[1][l] = ocol[1][l] + own.y;
+        ocol[2][l] = ocol[2][l] + own.z;
+      } else
+#endif
+      {
 #if DT_FIN_PARTIAL
       stack[fin_slot].a = own;
       stack[fin_slot].depth = -1;
@@ -2361,6 +2388,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       f.a = own; f.b = v3(0, 0, 0); f.k = 0; f.depth = -1; f.key = 0; f._pad = 0;
       stack[fin_slot] = f;
 #endif
+      }
     }
   }
 }
