@@ -10,7 +10,7 @@ O=$R/gpurun_out/prof_$TAG
 mkdir -p "$O"
 cd /tmp
 export TMPDIR=/tmp
-B="$R/bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline"
+B="$R/bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline --no-roofline"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt --output-format csv -- python3 $B > "$O/kt.log" 2>&1
 echo kt done
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$O/fetch" -o fetch --output-format csv -- python3 $B > "$O/fetch.log" 2>&1
