@@ -22,7 +22,7 @@ DT_OUT_SLAB = 1
 
 SHAPE_TYPES = {1: "sphere", 2: "cylinder", 3: "triangle", 4: "rectangle", 5: "rectprism_v2",
                6: "checkerboard", 7: "checkerboard_hole", 8: "checker_cylinder", 9: "rectprism_cyl"}
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class ShapeDesc(ctypes.Structure):
@@ -86,7 +86,7 @@ class Stats(ctypes.Structure):
                 ("reflect_errors", c_uint64), ("nan_pixels", c_uint64), ("tex_fetches", c_uint64),
                 ("stack_overflows", c_uint64), ("box_tests", c_uint64), ("prim_tests", c_uint64),
                 ("wave_node_visits", c_uint64), ("kernel_ms", c_double),
-                ("trace_kernel_ms", c_double)]
+                ("trace_kernel_ms", c_double), ("donations", c_uint64), ("donate_overflow", c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -27,6 +27,8 @@ extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_
 extern "C" const void* dt_trace_kernel_ptr(void);
 extern "C" hipError_t dt_launch_trace_rpc(const void* dev_launch, float* out, int grid, hipStream_t stream);
 extern "C" const void* dt_trace_kernel_rpc_ptr(void);
+extern "C" hipError_t dt_launch_trace_dn(const void* dev_launch, float* out, int grid, hipStream_t stream);
+extern "C" const void* dt_trace_kernel_dn_ptr(void);
 
 namespace {
 
@@ -52,12 +54,14 @@ struct HScene {
   const uint32_t* pl_cells; // primary-ray candidate lists (host_primlists.cpp)
   const uint32_t* pl_list;
   uint8_t* sky_miss;
+  void* dn_pool;
 };
 
 #define DT_N_STAMPS (64 + 3 * 8 * 256)   // diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters):
                                          // phases, then (waves, lanes, hits) per (light, shape) shadow test
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
-       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15, ST_N = 16 };
+       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15,
+       ST_DONATE = 16, ST_DN_OVF = 17, ST_N = 18 };
 
 int fail(int code, const std::string& msg)
 {
@@ -166,6 +170,8 @@ struct dt_scene {
   std::vector<double> pl_key;
   uint8_t* d_sky_miss = nullptr;   // 1-spp launches: missed-pixel flags (dt_sky_miss_kernel clears them)
   int64_t sky_miss_cap = 0;
+  void* d_dn_pool = nullptr;       // dt_trace_kernel_dn: DT_DN_POOL_REC work-sharing records per wave
+  int64_t dn_pool_waves = 0;
   PrimLists pl;
   bool pl_ok = false;
   void* d_pl_cells = nullptr;
@@ -309,7 +315,7 @@ static void release_device(dt_scene* s)
 {
   void** bufs[] = {&s->d_pl_cells, &s->d_pl_list, &s->d_nodes, &s->d_fnodes, &s->d_bnodes, &s->d_bparent,
                    &s->d_sg_cells, &s->d_sg_list, &s->d_leaf, &s->d_hdr, &s->d_geom, &s->d_mat, &s->d_lights,
-                   &s->d_tex, &s->d_zs, (void**)&s->d_stats, &s->d_launch, (void**)&s->d_sky_miss};
+                   &s->d_tex, &s->d_zs, (void**)&s->d_stats, &s->d_launch, (void**)&s->d_sky_miss, &s->d_dn_pool};
   for (void** b : bufs) {
     if (*b) (void)hipFree(*b);
     *b = nullptr;
@@ -324,6 +330,7 @@ static void release_device(dt_scene* s)
   s->h_zs = nullptr;
   s->zs_cap = 0;
   s->sky_miss_cap = 0;
+  s->dn_pool_waves = 0;
   s->copy_pending = s->timed = s->launched = false;
   s->pl_dirty = true;   // the primary lists go up again with the next upload
 }
@@ -632,13 +639,31 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   hs.pl_cells = (const uint32_t*)sc->d_pl_cells;
   hs.pl_list = (const uint32_t*)sc->d_pl_list;
   // scenes with a RectPrismWithCylinder take the trace kernel compiled with its tests (dt_kernels.hip
-  // DT_WITH_RPC), whose occupancy may differ
-  static int resident = 0, resident_rpc = 0;
+  // DT_WITH_RPC), whose occupancy may differ. DFS work sharing inside the wave (dt_trace_kernel_dn)
+  // when DT_DONATE=1; its pre-order paths hold 10 levels of 3 bits (max_depth <= 11, brdf_samples <= 6)
+  const char* dn_env = getenv("DT_DONATE");
+  const bool donate = !sc->no_cull && dn_env && dn_env[0] == '1' && P.max_depth <= 11 && P.brdf_samples <= 6;
+  static int resident = 0, resident_rpc = 0, resident_dn = 0;
   if (!resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
   if (sc->no_cull && !resident_rpc) resident_rpc = max_resident_waves(dt_trace_kernel_rpc_ptr(), 64);
-  const int64_t waves = sc->no_cull ? resident_rpc : resident;
+  if (donate && !resident_dn) resident_dn = max_resident_waves(dt_trace_kernel_dn_ptr(), 64);
+  const int64_t waves = sc->no_cull ? resident_rpc : donate ? resident_dn : resident;
   int64_t grid = P.n_items < waves ? P.n_items : waves;
   if (grid < 1) grid = 1;
+  hs.dn_pool = nullptr;
+  if (donate) {
+    if (grid > sc->dn_pool_waves) {
+      if (sc->d_dn_pool) {
+        HIPCHK(hipStreamSynchronize(st));
+        (void)hipFree(sc->d_dn_pool);
+        sc->d_dn_pool = nullptr;
+        sc->dn_pool_waves = 0;
+      }
+      HIPCHK(hipMalloc(&sc->d_dn_pool, (size_t)grid * DT_DN_POOL_REC * 32));
+      sc->dn_pool_waves = grid;
+    }
+    hs.dn_pool = sc->d_dn_pool;
+  }
   // two items per queue atomic pays when every wave takes many items (C3: ~500, +2%); with few
   // (C2: ~30) the coarser tail costs more (-11%)
   dtd::DParams PL = P;
@@ -666,6 +691,7 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
     PL.sky_defer = 1;
     hs.sky_miss = sc->d_sky_miss;
   }
+  PL.donate = donate ? 1 : 0;
   memset(sc->h_launch, 0, dt_launch_size());
   memcpy(sc->h_launch + dt_scene_struct_offset(), &hs, sizeof(hs));   // after every hs field is set
   memcpy(sc->h_launch + dt_params_struct_offset(), &PL, sizeof(PL));
@@ -676,7 +702,8 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 1 + DT_N_STAMPS), st));
   HIPCHK(hipEventRecord(sc->ev0, st));
   HIPCHK(sc->no_cull ? dt_launch_trace_rpc(sc->d_launch, out_dev, (int)grid, st)
-                     : dt_launch_trace(sc->d_launch, out_dev, (int)grid, st));
+         : donate   ? dt_launch_trace_dn(sc->d_launch, out_dev, (int)grid, st)
+                    : dt_launch_trace(sc->d_launch, out_dev, (int)grid, st));
   if (PL.sky_defer) HIPCHK(dt_launch_sky_miss(sc->d_launch, out_dev, n_px, st));
   HIPCHK(hipEventRecord(sc->ev1, st));
   sc->timed = true;
@@ -729,6 +756,8 @@ int dt_collect_stats(const dt_scene* sc_c, void* stream, dt_stats* stats)
   stats->box_tests = h[ST_BOX];
   stats->prim_tests = h[ST_PRIM];
   stats->wave_node_visits = h[ST_WNODES];
+  stats->donations = h[ST_DONATE];
+  stats->donate_overflow = h[ST_DN_OVF];
   if (sc->timed) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, sc->ev0, sc->ev1) == hipSuccess) {

@@ -68,8 +68,15 @@ using namespace dtd;
 #ifndef DT_WITH_RPC
 #define DT_WITH_RPC 0
 #endif
+// DT_DONATE=1 (a third compilation, build/dt_kernels_dn.o): dt_trace_kernel_dn, whose idle lanes take
+// whole pending subtrees from lanes with deep DFS trees (see "DFS work sharing" below)
+#ifndef DT_DONATE
+#define DT_DONATE 0
+#endif
 #if DT_WITH_RPC
 #define DT_TRACE_KERNEL dt_trace_kernel_rpc
+#elif DT_DONATE
+#define DT_TRACE_KERNEL dt_trace_kernel_dn
 #else
 #define DT_TRACE_KERNEL dt_trace_kernel
 #endif
@@ -124,7 +131,8 @@ using namespace dtd;
 #endif
 
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
-       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15, ST_N = 16 };
+       ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15,
+       ST_DONATE = 16, ST_DN_OVF = 17, ST_N = 18 };
 
 __constant__ uint32_t c_primes[10][3] = {
     {995615039u, 600173719u, 701464987u}, {831731269u, 162318869u, 136250887u},
@@ -167,6 +175,7 @@ struct DScene {
   const uint32_t* pl_cells; // primary-ray candidate lists (host_primlists.cpp): (first, count) per pixel block
   const uint32_t* pl_list;  // (fast-tree node, float bits of t_near) per entry
   uint8_t* sky_miss;        // P.sky_defer: per queue position, 1 when the pixel's sample missed
+  void* dn_pool;            // P.donate: DT_DN_POOL_REC records of 32 B per resident wave (DFS work sharing)
 };
 
 // pow(x, n) for the integer exponents the reference writes as pow(x, 2.0) etc. pow(x, 1) is x
@@ -1911,12 +1920,103 @@ __device__ __forceinline__ float schlick_complex(float cos_theta, float R0)
   return (float)((R0 + (1 - R0)) + pw5((double)(1 - cos_theta)));
 }
 
+// =====================================================================================
+// DFS work sharing (DT_DONATE, dt_trace_kernel_dn)
+// =====================================================================================
+// A deep glossy cascade keeps one lane of its wave busy for ~100 DFS steps while the other 63 are
+// done (at 8 ranks one such wave bounds a rank's kernel). Here a lane whose own sample
+// is finished takes a whole pending subtree (a NODE entry) from a lane that has more than one, and
+// runs it as a DFS of its own. The reference adds every node's own light to one accumulator in DFS
+// post-order; a subtree's additions are a contiguous run of that sequence, so the thief records its
+// colours in order in a list (records in global memory) and the owner, reaching the REPLAY marker
+// left in place of the entry, adds them one by one: the same additions in the same order, bit for
+// bit. A thief's own donations become SUBLIST records of its list, replayed in place. in_motion
+// (the last rayColor's, Q6) is kept as the value of the node with the largest pre-order path
+// (_pad: 3 bits per level, the call slot + 1), so it does not depend on who ran which node.
+#if DT_DONATE
+#define DN_BLK 16              // records per block; the last slot of a block links to the next
+#define DN_NBLK (DT_DN_POOL_REC / DN_BLK)
+#define DN_LIMIT (DN_NBLK / 2) // no new donation once this many blocks are in use
+enum { DN_COLOR = 1, DN_LINK = 2, DN_SUB = 3, DN_END = 4 };
+struct DnRec {
+  double x, y, z;
+  uint32_t tag;
+  uint32_t aux;                // LINK: next record; SUB: the sublist's first block; END: max pre-order path
+};
+struct DnCtx {
+  DnRec* pool;                 // this wave's records
+  unsigned* next;              // LDS: blocks handed out
+  unsigned* done;              // LDS: bit per block: the list starting there is complete
+  int* pair;                   // LDS: donor lane per pairing rank
+};
+// append a record to the list being filled at pos (chaining a new block when this one is full)
+__device__ __forceinline__ void dn_put(const DnCtx& dn, int& pos, double x, double y, double z, uint32_t tag,
+                                       uint32_t aux, unsigned long long* ovf)
+{
+  if ((pos & (DN_BLK - 1)) == DN_BLK - 1) {
+    const unsigned nb = atomicAdd(dn.next, 1u);
+    if (nb >= DN_NBLK) {
+      // pool full: the list ends here (an END record in the link slot, so its replay terminates);
+      // counted in dt_stats.donate_overflow, which the tests require to be zero
+      atomicAdd(ovf, 1ull);
+      DnRec& l = dn.pool[pos];
+      l.x = 0.0;
+      l.tag = DN_END;
+      l.aux = 0u;
+      return;
+    }
+    DnRec& l = dn.pool[pos];
+    l.tag = DN_LINK;
+    l.aux = nb * DN_BLK;
+    pos = (int)(nb * DN_BLK);
+  }
+  DnRec& r = dn.pool[pos];
+  r.x = x; r.y = y; r.z = z;
+  r.tag = tag;
+  r.aux = aux;
+  ++pos;
+}
+#define DT_ROOT_PAD 0
+#else
+#define DT_ROOT_PAD 1
+#endif
+
 // One full rayColor tree for the lanes with `active`. Appends to out.color in the
 // reference's accumulation order.
-__device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 org0, uint32_t rootkey, float shift,
+__device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, V3 org0, uint32_t rootkey, float shift_in,
                          PassOut& out, Entry* stack, Counters& cnt, double (*nrec)[DT_WAVE],
-                         double (*ocol)[DT_WAVE], float (*lsxy)[2][DT_WAVE])
+                         double (*ocol)[DT_WAVE], float (*lsxy)[2][DT_WAVE]
+#if DT_DONATE
+                         , const DnCtx& dn
+#endif
+                         )
 {
+#if DT_DONATE
+  // the sample whose node the lane works on: its own, or (a thief) the donor's
+  Ctx c = c_in;
+  float shift = shift_in;
+  int out_pos = -1;            // -1: own sample (colours into ocol); else the next record of the list being filled
+  int out_blk = 0;             // first block of that list (its done bit)
+  int npend = 0;               // NODE entries (depth > 0) on the lane's stack
+  int mk_o = -1, mk_t = -1;    // largest pre-order path seen: own sample / current list
+  bool mo_o = false, mo_t = false;   // its in_motion
+  const int lane_ = threadIdx.x & (DT_WAVE - 1);
+  if (lane_ == 0) *dn.next = 0;
+  for (int q = lane_; q < DN_NBLK / 32; q += DT_WAVE) dn.done[q] = 0u;
+  __syncthreads();
+  auto emit = [&](const V3& a) {   // a node's own light, in the reference's accumulation order
+    if (out_pos < 0) {
+      ocol[0][lane_] = ocol[0][lane_] + a.x;
+      ocol[1][lane_] = ocol[1][lane_] + a.y;
+      ocol[2][lane_] = ocol[2][lane_] + a.z;
+    } else {
+      dn_put(dn, out_pos, a.x, a.y, a.z, DN_COLOR, 0u, c.S->stats + ST_DN_OVF);
+    }
+  };
+#else
+  const Ctx& c = c_in;
+  const float shift = shift_in;
+#endif
   const DScene& S = *c.S;
   const DParams& P = *c.P;
   int sp = 0;
@@ -1925,15 +2025,141 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
 #endif
   if (active && P.max_depth > 0) {
     Entry e;
-    e.a = ray0; e.b = org0; e.k = 1.0f; e.depth = P.max_depth; e.key = rootkey; e._pad = 1;  // root
+    e.a = ray0; e.b = org0; e.k = 1.0f; e.depth = P.max_depth; e.key = rootkey; e._pad = DT_ROOT_PAD;  // root
     stack[sp++] = e;
+#if DT_DONATE
+    npend = 1;
+#endif
   }
   while (true) {
     DT_T(t0);
+#if DT_DONATE
+    // ---- work sharing: a free lane (own sample finished, no list open) takes the bottom-most
+    // pending NODE of a lane that has two or more (the one processed last: the most overlap) ----
+    if (P.donate) {
+      const bool free_l = sp == 0 && out_pos < 0;
+      const bool donor = npend >= 2 && *dn.next < DN_LIMIT;
+      const unsigned long long fm = __ballot(free_l), dm = __ballot(donor);
+      if (fm && dm) {
+        const int np = min(__popcll(fm), __popcll(dm));
+        const int rf = __popcll(fm & ((1ull << lane_) - 1)), rd = __popcll(dm & ((1ull << lane_) - 1));
+        const bool give = donor && rd < np, take = free_l && rf < np;
+        if (give) dn.pair[rd] = lane_;
+        __syncthreads();
+        const int src = take ? dn.pair[rf] : lane_;
+        __syncthreads();
+        Entry de;
+        de.a = v3(0, 0, 0); de.b = v3(0, 0, 0); de.k = 0; de.depth = 0; de.key = 0; de._pad = 0;
+        uint32_t blk = 0;
+        if (give) {
+          int b = 0;
+          while (stack[b].depth <= 0) ++b;   // npend >= 2: a NODE entry exists below the top
+          de = stack[b];
+          blk = atomicAdd(dn.next, 1u);
+          stack[b].depth = -2;               // REPLAY the list that starts at block blk
+          stack[b].key = blk;
+          --npend;
+          atomicAdd(S.stats + ST_DONATE, 1ull);
+        }
+        // move the entry and the donor's sample identity (RNG pixel/sample, blur shift) to the thief
+        const int* ew = (const int*)&de;
+        int tw[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) tw[q] = __shfl(ew[q], src, DT_WAVE);
+        const uint32_t tblk = (uint32_t)__shfl((int)blk, src, DT_WAVE);
+        const uint32_t tpix = (uint32_t)__shfl((int)c.rng.pixel, src, DT_WAVE);
+        const uint32_t tsmp = (uint32_t)__shfl((int)c.rng.sample, src, DT_WAVE);
+        const float tsh = __int_as_float(__shfl(__float_as_int(shift), src, DT_WAVE));
+        if (take) {
+          Entry te;
+          int* tv = (int*)&te;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) tv[q] = tw[q];
+          stack[0] = te;
+          sp = 1;
+          npend = 1;
+          out_blk = (int)tblk;
+          out_pos = (int)(tblk * DN_BLK);
+          c.rng.pixel = tpix;
+          c.rng.sample = tsmp;
+          shift = tsh;
+          mk_t = -1;
+          mo_t = false;
+        }
+      }
+    }
+#endif
     // pop FINISH entries (own-light contributions), then the next NODE
     bool have = false;
+#if DT_DONATE
+    bool waiting = false;   // a donated subtree's list is not complete yet
+#endif
     Entry e;
     int pidx = 0;   // DT_LAZY_ENTRY: the popped NODE entry's slot
+#if DT_DONATE
+    while (sp > 0) {
+      const int d = stack[--sp].depth;
+      if (d == -1) {
+        emit(stack[sp].a);
+      } else if (d > 0) {
+        pidx = sp;
+        have = true;
+        --npend;
+        break;
+      } else if (d <= -2) {   // a donated subtree: REPLAY its list (-2), or CONTINUE replaying it (-3)
+        const uint32_t blk = stack[sp].key;
+        if (out_pos >= 0) {    // filling a list ourselves: splice the sublist in, replayed in place later
+          dn_put(dn, out_pos, 0.0, 0.0, 0.0, DN_SUB, blk, S.stats + ST_DN_OVF);
+          continue;
+        }
+        if (!(dn.done[blk >> 5] & (1u << (blk & 31)))) {   // its thief is still at it: wait
+          ++sp;
+          waiting = true;
+          break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the records were written by another lane
+        int pos = d == -2 ? (int)(blk * DN_BLK) : (int)__float_as_uint(stack[sp].k);
+        while (true) {
+          const DnRec r = dn.pool[pos];
+          if (r.tag == DN_COLOR) {
+            ocol[0][lane_] = ocol[0][lane_] + r.x;
+            ocol[1][lane_] = ocol[1][lane_] + r.y;
+            ocol[2][lane_] = ocol[2][lane_] + r.z;
+            ++pos;
+          } else if (r.tag == DN_LINK) {
+            pos = (int)r.aux;
+          } else if (r.tag == DN_SUB) {
+            // the rest of this list after the sublist: CONTINUE here, the sublist's REPLAY above it
+            stack[sp].depth = -3;
+            stack[sp].k = __uint_as_float((uint32_t)(pos + 1));
+            ++sp;
+            if (sp < DT_STACK_MAX) {
+              stack[sp].depth = -2;
+              stack[sp].key = r.aux;
+              ++sp;
+            } else {
+              atomicAdd(S.stats + ST_STACK, 1ull);
+            }
+            break;
+          } else {   // DN_END: the list's (largest pre-order path, in_motion)
+            if ((int)r.aux >= mk_o) { mk_o = (int)r.aux; mo_o = r.x != 0.0; }
+            break;
+          }
+        }
+      }
+      // d == 0: an exhausted glossy sample's no-op entry
+    }
+    if (out_pos >= 0 && sp == 0 && !have) {
+      // a thief's subtree is done: close its list, then it is free again (its own identity back)
+      dn_put(dn, out_pos, mo_t ? 1.0 : 0.0, 0.0, 0.0, DN_END, (uint32_t)mk_t, S.stats + ST_DN_OVF);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      atomicOr(&dn.done[(uint32_t)out_blk >> 5], 1u << ((uint32_t)out_blk & 31));
+      out_pos = -1;
+      c.rng = c_in.rng;
+      shift = shift_in;
+    }
+    if (!__ballot(have || waiting)) break;
+#else
     while (sp > 0) {
 #if DT_FIN_PARTIAL
       // read the depth word first: a FINISH entry only carries its colour
@@ -1967,6 +2193,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
 #endif
     }
     if (!__ballot(have)) break;
+#endif
     DT_CNT(7);
 #if DT_PRIO_STEPS > 0
     // A deep glossy cascade (fan-out 2 per bounce, ~100 DFS steps for one lane against ~1.5 on
@@ -1993,15 +2220,24 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
 #define DT_EF_K k
 #endif
     V3 ray = DT_EF(a), eye = DT_EF(b);
-    const bool is_root = have && DT_EF(_pad) == 1;
+    const bool is_root = have && DT_EF(_pad) == DT_ROOT_PAD;
 #else
     V3 ray = e.a, eye = e.b;
     const int depth = e.depth;
     const float k = e.k;
     const uint32_t node = e.key;
-    const bool is_root = have && e._pad == 1;
+    const bool is_root = have && e._pad == DT_ROOT_PAD;
 #endif
+#if DT_DONATE
+    // in_motion of the node with the largest pre-order path so far (own sample / current list)
+    if (have) {
+      const int path = DT_EF(_pad);
+      if (out_pos < 0) { if (path >= mk_o) { mk_o = path; mo_o = false; } }
+      else if (path >= mk_t) { mk_t = path; mo_t = false; }
+    }
+#else
     if (have) out.in_motion = false;   // cpp:519
+#endif
     DT_WCNT(WC_RAYS, have);
 
     DT_T(t1);
@@ -2054,7 +2290,16 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       normal = shape_norm(hd.type, hd.flags, g, isectP, shift, S.stats + ST_PRISM, h.ccol);
       in = normalized(ray);
       shape_color = h.ccol >= 0 ? G3(g, h.ccol) : v3a(M.color);
+#if DT_DONATE
+      {
+        const bool mv = (M.flags & DT_F_MOTION) != 0;
+        const int path = DT_EF(_pad);
+        if (out_pos < 0) { if (path == mk_o) mo_o = mv; }
+        else if (path == mk_t) mo_t = mv;
+      }
+#else
       out.in_motion = (M.flags & DT_F_MOTION) != 0;
+#endif
       if (dot(mul(1e4, in), normal) >= 0) normal = mul(-1, normal);   // fixNorm
 
       // reserve the FINISH slot below the children
@@ -2072,6 +2317,17 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
         // leaves a depth-0 entry, which pops as a no-op (a depth-0 rayColor returns at once).
         // At depth 1 the children would return immediately: none are generated.
         if (depth - 1 > 0) {
+#if DT_DONATE
+          // pre-order path of a child: the parent's, plus its call slot + 1 at the child's level (3 bits
+          // per level from bit 27 down; host: max_depth <= 11, brdf_samples <= 6)
+          const int cpath_base = DT_EF(_pad);
+          const int cpath_shift = 30 - 3 * (P.max_depth - depth + 1);
+#define DT_CPATH(d) (cpath_base | ((d) << cpath_shift))
+#define DT_NPEND(cond) (npend += (cond) ? 1 : 0)
+#else
+#define DT_CPATH(d) 0
+#define DT_NPEND(cond) ((void)0)
+#endif
           V3 refl_ray = sub(in, mul(2 * dot(normal, in), normal));
           const double rn = dot(refl_ray, normal);
           int nref = 0;
@@ -2105,8 +2361,9 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
                 k_refl = (float)(0.5 * (pw2((double)rp) + pw2((double)rs)));
                 k_refr = 1 - k_refl;
                 Entry ch; ch.a = outr; ch.b = adj_org; ch.k = k_refr * k; ch.depth = depth - 1;
-                ch.key = child_key(node, 0); ch._pad = 0;
+                ch.key = child_key(node, 0); ch._pad = DT_CPATH(1);
                 stack[sp++] = ch;
+                DT_NPEND(1);
               }
             }
             if (nref > 0 && glossy && !P.nogloss) {
@@ -2155,14 +2412,16 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
                 if (exhausted) atomicAdd(S.stats + ST_GLOSSY, 1ull);
                 Entry ch; ch.a = sample_refl; ch.b = add(isectP, mul(eps, sample_refl));
                 ch.k = kg; ch.depth = exhausted ? 0 : depth - 1; ch.key = child_key(node, 2 + i);
-                ch._pad = 0;
+                ch._pad = DT_CPATH(2 + i);
                 stack[base + nref - 1 - i] = ch;
+                DT_NPEND(!exhausted);
               }
             } else if (nref > 0) {
               DT_WK(DT_WK_MIRROR, true);
               Entry ch; ch.a = refl_ray; ch.b = add(isectP, mul(eps, refl_ray)); ch.k = k_refl * k;
-              ch.depth = depth - 1; ch.key = child_key(node, 1); ch._pad = 0;
+              ch.depth = depth - 1; ch.key = child_key(node, 1); ch._pad = DT_CPATH(2);
               stack[base] = ch;
+              DT_NPEND(1);
             }
           }
         }
@@ -2373,10 +2632,14 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
         // no children were pushed: the FINISH entry would be the very next pop, so the own light
         // goes into the accumulator now, in the same order, without a stack round trip
         sp = fin_slot;
+#if DT_DONATE
+        emit(own);
+#else
         const int l = threadIdx.x & (DT_WAVE - 1);
         ocol[0][l] = ocol[0][l] + own.x;
         ocol[1][l] = ocol[1][l] + own.y;
         ocol[2][l] = ocol[2][l] + own.z;
+#endif
       } else
 #endif
       {
@@ -2391,6 +2654,9 @@ __device__ __forceinline__ void run_pass(const Ctx& c, bool active, V3 ray0, V3 
       }
     }
   }
+#if DT_DONATE
+  out.in_motion = mo_o;
+#endif
 }
 
 
@@ -2496,6 +2762,17 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   cnt.cur_path = 0;
 #endif
 
+#if DT_DONATE
+  __shared__ unsigned dn_next;
+  __shared__ unsigned dn_done[DN_NBLK / 32];
+  __shared__ int dn_pair[DT_WAVE];
+  DnCtx dn;
+  dn.pool = (DnRec*)S.dn_pool + (size_t)blockIdx.x * DT_DN_POOL_REC;
+  dn.next = &dn_next;
+  dn.done = dn_done;
+  dn.pair = dn_pair;
+#endif
+
   int64_t item = 0, batch_end = 0;
   while (true) {
     // items are dequeued DT_ITEM_BATCH at a time (one same-address atomic per batch)
@@ -2563,7 +2840,11 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         ocol[0][lane] = 0; ocol[1][lane] = 0; ocol[2][lane] = 0;
         po.hit = pass > 0;
         po.in_motion = false;
-        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt, nrec, ocol, lsxy);
+        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt, nrec, ocol, lsxy
+#if DT_DONATE
+                 , dn
+#endif
+                 );
         po.color = v3(ocol[0][lane], ocol[1][lane], ocol[2][lane]);
         if (pass == 0) {
           tmp_color = po.color;
@@ -2675,7 +2956,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   }
 }
 
-#if !DT_WITH_RPC
+#if !DT_WITH_RPC && !DT_DONATE
 // The sky of the pixels a 1-spp trace launch flagged as missed (P.sky_defer): renderImage's miss
 // branch (cpp:1074-1092: cloudColor of mcam * focalPoint) one pixel per lane, at the occupancy of a
 // small kernel instead of inside the trace kernel's register budget. With one sample the pixel is
@@ -2800,6 +3081,13 @@ extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_
   return hipGetLastError();
 }
 extern "C" const void* dt_trace_kernel_ptr(void) { return (const void*)dt_trace_kernel; }
+#elif DT_DONATE   // the trace kernel with DFS work sharing inside the wave
+extern "C" hipError_t dt_launch_trace_dn(const void* dev_launch, float* out, int grid, hipStream_t stream)
+{
+  hipLaunchKernelGGL(dt_trace_kernel_dn, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
+  return hipGetLastError();
+}
+extern "C" const void* dt_trace_kernel_dn_ptr(void) { return (const void*)dt_trace_kernel_dn; }
 #else   // DT_WITH_RPC: the trace kernel for scenes with a RectPrismWithCylinder
 extern "C" hipError_t dt_launch_trace_rpc(const void* dev_launch, float* out, int grid, hipStream_t stream)
 {

@@ -107,6 +107,7 @@ enum { RP_LB = 0, RP_UB = 3, RP_NBOT = 6, RP_NRIGHT = 9, RP_NFRONT = 12, RP_A = 
        RP_ADC = 24, RP_NADC = 27, RP_D = 30, RP_NH = 33, RP_H = 34 };
 enum { RH_C1 = 0, RH_C2 = 3, RH_AX = 6, RH_R2 = 9, RH_COL = 10, RH_C1A = 13, RH_C2A = 14, RH_SIZE = 15 };
 
+#define DT_DN_POOL_REC 8192    // DFS work-sharing records (32 B) per resident wave (dt_trace_kernel_dn)
 #define DT_MAX_SGRID 16        // lights with a shadow grid (host_shadowgrid.cpp)
 #define DT_SGRID_MAX_LIST 96   // longer candidate lists: the cell walks the tree instead
 #define DT_SG_REACH_DEFAULT 0.25f   // a cell's list covers points this many cells outside it
@@ -148,6 +149,7 @@ struct DParams {
                           // outside its box (host: no shadow grid, no primary lists either)
   int32_t bump_up_only;   // the bump tree / blur-padded lists were built for shifts >= 0 only (host_accel.cpp):
                           // a lane with a negative shift sends its wave to the reference-tree walk
+  int32_t donate;         // dt_trace_kernel_dn: idle lanes take pending DFS subtrees of other lanes
   uint32_t seed;
   float aperture, focal_length, near_plane;
   float l, r, t, b;

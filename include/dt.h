@@ -39,7 +39,8 @@ extern "C" {
 /* 2: dt_tiles ownership by hashed tile groups (dtd::tile_of) with equal-size slabs,
  *    dt_scene_prepare / dt_scene_upload / dt_accel_info_build, RectPrismWithCylinder
  *    (DT_SHAPE_RECTPRISM_CYL with the dt_scene_desc.holes array) */
-#define DT_ABI_VERSION 2
+/* 3: dt_stats.donations / donate_overflow (DFS work sharing inside a wave, DT_DONATE) */
+#define DT_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------- */
 #define DT_OK              0
@@ -236,6 +237,8 @@ typedef struct dt_stats {
   uint64_t wave_node_visits;  /* wave-level BVH node visits        0 otherwise)  */
   double   kernel_ms;         /* device time of the render kernels (hipEvents, same stream) */
   double   trace_kernel_ms;   /* device time of the dominant (trace) kernel alone */
+  uint64_t donations;         /* pending DFS subtrees run by another lane of the wave (work sharing) */
+  uint64_t donate_overflow;   /* work-sharing records dropped (per-wave pool full); 0 when validated */
 } dt_stats;
 
 /* ---- API ------------------------------------------------------------------ */

@@ -1,0 +1,58 @@
+"""DFS work sharing inside a wave (dt_kernels.hip DT_DONATE, dt_trace_kernel_dn; DT_DONATE=1).
+
+Idle lanes run whole pending subtrees of other lanes' rayColor trees and the owners replay the
+recorded colours in the reference's accumulation order, so the image must be bit-identical to the
+product kernel's (and the oracle's) with the same rays traced. The cases are the ones that donate:
+a C3 share of the 8-way tile split (the deep glossy column), C5's room-to-tunnel transition frame
+(8 rays per sample), a motion-blur frame (in_motion, Q6, is the last rayColor's: kept as the
+value of the largest pre-order path, whoever ran that node) and C2's full frame.
+"""
+import numpy as np
+import pytest
+import torch
+
+import distraytracer_amd as dt
+import oracle
+from test_gpu_configs import _globals
+
+pytestmark = pytest.mark.gpu
+
+
+def _render(g, built, frame, tile, donate, monkeypatch):
+    monkeypatch.setenv("DT_DONATE", "1" if donate else "0")
+    scene = dt.Scene(built, g)
+    n = dt.slab_floats(g, tile) if tile.layout == dt.DT_OUT_SLAB else 3 * g.xRes * g.yRes
+    out = torch.zeros(n, dtype=torch.float32, device="cuda")
+    st = dt.render(scene, g, frame, out, tile)
+    scene.close()
+    return out.cpu().numpy(), st
+
+
+CASES = [  # (id, builder args, frame, tile world, oracle check)
+    ("c3_rank0_of_8", ("final", 240, 0, 1920, 1080, 64, 8), 240, 8, True),
+    ("c5_1088_transition", ("final", 1088, 0, 3840, 2160, 64, 10), 1088, 512, True),
+    ("c5_1920_blur", ("final", 1920, 0, 3840, 2160, 64, 10), 1920, 512, True),
+    ("c2_full", ("final", 240, 0, 800, 600, 16, 4), 240, 1, False),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_donate_bit_identical(cuda, monkeypatch, case):
+    label, args, frame, world, check_oracle = case
+    g, built = _globals(*args)
+    tile = dt.tiles(rank=0, world=world, layout=dt.DT_OUT_SLAB) if world > 1 else dt.tiles()
+    base, st0 = _render(g, built, frame, tile, False, monkeypatch)
+    img, st = _render(g, built, frame, tile, True, monkeypatch)
+    print("%s: donations=%d overflow=%d kernel %.2f -> %.2f ms" % (label, st.donations, st.donate_overflow,
+                                                                 st0.trace_kernel_ms, st.trace_kernel_ms))
+    assert st0.donations == 0
+    assert st.donate_overflow == 0 and st.stack_overflows == 0
+    assert st.rays == st0.rays and st.shadow_rays == st0.shadow_rays and st.samples == st0.samples
+    assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), \
+        "%s: %d channels differ" % (label, int((img != base).sum()))
+    if label != "c2_full":
+        assert st.donations > 0   # the deep cascades did donate
+    if check_oracle:
+        ref, rst = oracle.render(built, g, frame, tile, out=np.zeros(img.size, dtype=np.float32))
+        assert st.rays == rst.rays
+        assert float(np.abs(img.astype(np.float64) - ref.astype(np.float64)).max()) <= 1e-4
