@@ -2000,6 +2000,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
   int npend = 0;               // NODE entries (depth > 0) on the lane's stack
   int mk_o = -1, mk_t = -1;    // largest pre-order path seen: own sample / current list
   bool mo_o = false, mo_t = false;   // its in_motion
+  int dn_steps = 0;
   const int lane_ = threadIdx.x & (DT_WAVE - 1);
   if (lane_ == 0) *dn.next = 0;
   for (int q = lane_; q < DN_NBLK / 32; q += DT_WAVE) dn.done[q] = 0u;
@@ -2036,7 +2037,8 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
 #if DT_DONATE
     // ---- work sharing: a free lane (own sample finished, no list open) takes the bottom-most
     // pending NODE of a lane that has two or more (the one processed last: the most overlap) ----
-    if (P.donate) {
+    // only once the pass has run P.donate_after steps: the common item (1.5 steps) never pays for it
+    if (P.donate && ++dn_steps > P.donate_after) {
       const bool free_l = sp == 0 && out_pos < 0;
       const bool donor = npend >= 2 && *dn.next < DN_LIMIT;
       const unsigned long long fm = __ballot(free_l), dm = __ballot(donor);

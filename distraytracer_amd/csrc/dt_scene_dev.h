@@ -150,6 +150,7 @@ struct DParams {
   int32_t bump_up_only;   // the bump tree / blur-padded lists were built for shifts >= 0 only (host_accel.cpp):
                           // a lane with a negative shift sends its wave to the reference-tree walk
   int32_t donate;         // dt_trace_kernel_dn: idle lanes take pending DFS subtrees of other lanes
+  int32_t donate_after;   // ... once a pass has run this many DFS steps
   uint32_t seed;
   float aperture, focal_length, near_plane;
   float l, r, t, b;

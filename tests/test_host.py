@@ -340,3 +340,24 @@ def test_accel_info_matches_scene_bvh():
                                  ctypes.byref(ni)), "dt_bvh_build")
     assert info["n_nodes"] == nn.value
     assert info["boxes_ordered"] == 1 and info["n_fnodes"] == info["n_nodes"]
+
+
+def test_work_header_and_oracle_counts():
+    """SURVEY §8(d)'s work unit: include/dt_work.h parsed by distraytracer_amd/work.py (the weights
+    bench.py prices with), and the oracle's reference-loop counts on a small C2-like render: one
+    camera event per sample, one light event per shadow ray, counting leaves the image unchanged."""
+    from distraytracer_amd import work
+    assert work.N_EVENTS == 35 and len(work.WEIGHTS) == work.N_EVENTS and work.PEAK_FP64_TFLOPS == 78.6
+    assert work.NAMES[0] == "box" and work.NAMES[work.SKY] == "sky"
+    assert work.NAMES[1 + 4] == "hit_shape.rectangle" and work.NAMES[23 + 2] == "brdf.cook_torrance"
+    g, b = final240()
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = 40, 24, 4, 4
+    tile = dt.tiles()
+    img, st, wk = oracle.render_work(b, g, 240, tile)
+    ref, _ = oracle.render(b, g, 240, tile)
+    assert np.array_equal(img, ref)
+    n = dict(zip(work.NAMES, wk.tolist()))
+    assert n["camera"] == st.samples == 40 * 24 * 4
+    assert n["light"] == st.shadow_rays and n["hit"] <= st.rays and n["box"] > 0
+    assert n["sky"] >= st.sky_pixels   # the reference loop marches once per missing sample
+    assert work.price(wk) == pytest.approx(sum(float(c) * w for c, w in zip(wk, work.WEIGHTS)))

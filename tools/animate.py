@@ -16,6 +16,12 @@ all stay zero over the run.
 
 Frames >= frame_cloud (n >= 244) force 1 spp and no aperture, as buildFinal does
 (scene.h:795-796); the reported samples are the ones actually rendered.
+
+--donate auto (default): frames whose rays fan out into deep glossy cascades render with the
+  work-sharing trace kernel (DT_DONATE=1), the others with the product kernel. The
+  choice comes from a probe render of a 1/1024 tile share of the frame itself (a few ms): more
+  than --donate-rps rays per sample (default 3.5; C3 has 1.46, the tunnel's blur frames 2.8, the
+  transition frames up to 8.1) selects work sharing. --donate on|off forces one kernel.
 """
 import argparse
 import json
@@ -32,7 +38,7 @@ sys.path.insert(0, ROOT)
 # points (geometry.cpp:890-919) are not among them: the reference prints and returns the nearest face
 # normal, and so does the device; they are reported as prism_norm_fallback.
 ABORT_COUNTERS = ("stack_overflows", "nan_pixels", "uv_out_of_range", "glossy_exhausted", "reflect_errors",
-                  "spherelight_exhausted")
+                  "spherelight_exhausted", "donate_overflow")
 REPORTED = ABORT_COUNTERS + ("prism_norm_fallback",)
 
 
@@ -58,6 +64,8 @@ def main():
     ap.add_argument("--split", default="frames", choices=("frames", "tiles", "static"))
     ap.add_argument("--out", default="", help="directory for frame.NNNN.png (none: keep on the GPU)")
     ap.add_argument("--per-frame", action="store_true", help="print host-build and render ms per frame (stderr)")
+    ap.add_argument("--donate", default="auto", choices=("auto", "on", "off"))
+    ap.add_argument("--donate-rps", type=float, default=3.5)
     args = ap.parse_args()
 
     import torch
@@ -116,6 +124,23 @@ def main():
         pipe = GatherPipeline(split, [z(split.slab_floats), z(split.slab_floats)],
                               [z(world * split.slab_floats if rank == 0 else 1) for _ in range(2)], img)
     sh = torch.cuda.current_stream(dev).cuda_stream
+    g_res = dt.globals_default()
+    g_res.xRes, g_res.yRes = W, H
+    probe_tile = dt.tiles(rank=0, world=1024, layout=dt.DT_OUT_SLAB)
+    probe = torch.empty(max(dt.slab_floats(g_res, probe_tile), 1), dtype=torch.float32, device=dev)
+    donated = 0
+
+    def choose_kernel(scene, g, n):
+        """DT_DONATE for frame n's render: the probe's rays per sample decide (--donate auto)"""
+        if args.donate != "auto":
+            os.environ["DT_DONATE"] = "1" if args.donate == "on" else "0"
+            return args.donate == "on", None
+        os.environ["DT_DONATE"] = "0"
+        pst = dt.render(scene, g, n * 8, probe, probe_tile)
+        rps = pst.rays / max(pst.samples, 1)
+        on = rps > args.donate_rps
+        os.environ["DT_DONATE"] = "1" if on else "0"
+        return on, rps
     # frame n+1's host build runs on a worker thread while frame n renders (ctypes releases the
     # GIL inside the library calls)
     with ThreadPoolExecutor(1) as ex:
@@ -126,6 +151,8 @@ def main():
             fut = next_job(ex)
             f1 = time.perf_counter()
             scene.upload()   # device half (a few ms), between renders
+            dn_on, probe_rps = choose_kernel(scene, g, n)
+            donated += dn_on
             if pipe is None:
                 st = dt.render(scene, g, n * 8, img)
             else:
@@ -141,6 +168,8 @@ def main():
             if args.per_frame:
                 rec = {"n": n, "frame": n * 8, "rank": rank, "host_ms": round(host_s * 1e3, 1),
                        "render_ms": round((f2 - f1) * 1e3, 1), "spp": st.samples // max(st.pixels, 1),
+                       "donate": bool(dn_on), "probe_rays_per_sample": probe_rps and round(probe_rps, 3),
+                       "donations": st.donations, "donate_overflow": st.donate_overflow,
                        "rays_per_sample": round(st.rays / max(st.samples, 1), 3), "sky_pixels": st.sky_pixels}
                 rec.update({key: getattr(st, key) for key in REPORTED})
                 print(json.dumps(rec), file=sys.stderr, flush=True)
@@ -177,7 +206,9 @@ def main():
                                           "static": "frame-parallel, frame n on rank n %% %d" % world,
                                           "tiles": "tile-split x%d + RCCL gather per frame" % world}[args.split],
                           "abort_counters": {k: aborts[k] for k in ABORT_COUNTERS},
-                          "prism_norm_fallback": aborts["prism_norm_fallback"]}), flush=True)
+                          "prism_norm_fallback": aborts["prism_norm_fallback"],
+                          "work_sharing": {"mode": args.donate, "rays_per_sample_above": args.donate_rps,
+                                           "frames_on_rank0": donated}}), flush=True)
     if distributed:
         dist.destroy_process_group()
     if any(aborts[k] for k in ABORT_COUNTERS):
