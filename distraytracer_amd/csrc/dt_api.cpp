@@ -693,7 +693,7 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   }
   PL.donate = donate ? 1 : 0;
   const char* dn_after = getenv("DT_DONATE_AFTER");
-  PL.donate_after = dn_after ? atoi(dn_after) : 4;
+  PL.donate_after = dn_after ? atoi(dn_after) : 2;
   memset(sc->h_launch, 0, dt_launch_size());
   memcpy(sc->h_launch + dt_scene_struct_offset(), &hs, sizeof(hs));   // after every hs field is set
   memcpy(sc->h_launch + dt_params_struct_offset(), &PL, sizeof(PL));

@@ -19,9 +19,10 @@ Frames >= frame_cloud (n >= 244) force 1 spp and no aperture, as buildFinal does
 
 --donate auto (default): frames whose rays fan out into deep glossy cascades render with the
   work-sharing trace kernel (DT_DONATE=1), the others with the product kernel. The
-  choice comes from a probe render of a 1/1024 tile share of the frame itself (a few ms): more
-  than --donate-rps rays per sample (default 3.5; C3 has 1.46, the tunnel's blur frames 2.8, the
-  transition frames up to 8.1) selects work sharing. --donate on|off forces one kernel.
+  choice comes from a probe render of a 1/256 tile share of the frame itself (~0.5% of the
+  frame): more than --donate-rps rays per sample (default 2.5; C3 has 1.46 and the kernel costs it
+  ~5%, the transition frames from 3.0 up to 8.1 gain 0-18%, profiles/r03j_*) selects work
+  sharing. --donate on|off forces one kernel.
 """
 import argparse
 import json
@@ -65,7 +66,7 @@ def main():
     ap.add_argument("--out", default="", help="directory for frame.NNNN.png (none: keep on the GPU)")
     ap.add_argument("--per-frame", action="store_true", help="print host-build and render ms per frame (stderr)")
     ap.add_argument("--donate", default="auto", choices=("auto", "on", "off"))
-    ap.add_argument("--donate-rps", type=float, default=3.5)
+    ap.add_argument("--donate-rps", type=float, default=2.5)
     args = ap.parse_args()
 
     import torch
@@ -126,7 +127,7 @@ def main():
     sh = torch.cuda.current_stream(dev).cuda_stream
     g_res = dt.globals_default()
     g_res.xRes, g_res.yRes = W, H
-    probe_tile = dt.tiles(rank=0, world=1024, layout=dt.DT_OUT_SLAB)
+    probe_tile = dt.tiles(rank=0, world=256, layout=dt.DT_OUT_SLAB)
     probe = torch.empty(max(dt.slab_floats(g_res, probe_tile), 1), dtype=torch.float32, device=dev)
     donated = 0
 
