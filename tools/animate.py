@@ -20,9 +20,10 @@ Frames >= frame_cloud (n >= 244) force 1 spp and no aperture, as buildFinal does
 --donate auto (default): frames whose rays fan out into deep glossy cascades render with the
   work-sharing trace kernel (DT_DONATE=1), the others with the product kernel. The
   choice comes from a probe render of a 1/256 tile share of the frame itself (~0.5% of the
-  frame): more than --donate-rps rays per sample (default 2.5; C3 has 1.46 and the kernel costs it
-  ~5%, the transition frames from 3.0 up to 8.1 gain 0-18%, profiles/r03j_*) selects work
-  sharing. --donate on|off forces one kernel.
+  frame): more than --donate-rps rays per sample (default 3.1) selects work sharing. Measured over
+  all 300 frames (profiles/r03k_c5_full_*.log): frames below ~3.1 rays per sample (C3 1.46, the
+  room frames, the tunnel's blur frames at 2.8) lose 1-5% with it, the transition frames from 3.2
+  up to 8.1 gain 2-17%. --donate on|off forces one kernel.
 """
 import argparse
 import json
@@ -66,7 +67,7 @@ def main():
     ap.add_argument("--out", default="", help="directory for frame.NNNN.png (none: keep on the GPU)")
     ap.add_argument("--per-frame", action="store_true", help="print host-build and render ms per frame (stderr)")
     ap.add_argument("--donate", default="auto", choices=("auto", "on", "off"))
-    ap.add_argument("--donate-rps", type=float, default=2.5)
+    ap.add_argument("--donate-rps", type=float, default=3.1)
     args = ap.parse_args()
 
     import torch
