@@ -28,6 +28,7 @@ extern "C" const void* dt_trace_kernel_ptr(void);
 extern "C" hipError_t dt_launch_trace_rpc(const void* dev_launch, float* out, int grid, hipStream_t stream);
 extern "C" const void* dt_trace_kernel_rpc_ptr(void);
 extern "C" hipError_t dt_launch_trace_dn(const void* dev_launch, float* out, int grid, hipStream_t stream);
+extern "C" hipError_t dt_launch_normalize(const double* in, double* out, int64_t n, hipStream_t stream);
 extern "C" const void* dt_trace_kernel_dn_ptr(void);
 
 namespace {
@@ -980,5 +981,27 @@ extern "C" int dt_debug_counters(const dt_scene* sc, uint64_t* out, int32_t n)
   std::vector<unsigned long long> h(ST_N + 1 + DT_N_STAMPS);
   HIPCHK(hipMemcpy(h.data(), sc->d_stats, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
   for (int i = 0; i < n; ++i) out[i] = h[ST_N + 1 + i];
+  return DT_OK;
+}
+
+extern "C" int dt_debug_normalize(const double* in, double* out, int64_t n)
+{
+  if (!in || !out || n < 0 || n > (int64_t)1 << 28) return fail(DT_E_INVALID, "bad arguments");
+  if (n == 0) return DT_OK;
+  int dev_count = 0;
+  if (hipGetDeviceCount(&dev_count) != hipSuccess || dev_count < 1) return fail(DT_E_NO_DEVICE, "no HIP device");
+  const size_t bytes = (size_t)n * 3 * sizeof(double);
+  double *din = nullptr, *dout = nullptr;
+  if (hipMalloc((void**)&din, bytes) != hipSuccess) return fail(DT_E_OOM, "hipMalloc");
+  if (hipMalloc((void**)&dout, bytes) != hipSuccess) {
+    (void)hipFree(din);
+    return fail(DT_E_OOM, "hipMalloc");
+  }
+  hipError_t e = hipMemcpy(din, in, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = dt_launch_normalize(din, dout, n, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
+  (void)hipFree(din);
+  (void)hipFree(dout);
+  if (e != hipSuccess) return fail(DT_E_NO_DEVICE, std::string("HIP: ") + hipGetErrorString(e));
   return DT_OK;
 }

@@ -3051,7 +3051,24 @@ extern "C" __global__ void dt_unpack_kernel(const DLaunch* __restrict__ Lp, int 
   image[off + 2] = s[2];
 }
 
+// the kernels' vector normalisation (dt_math.h normalized) on n vectors: the numerics check of
+// its shared-reciprocal division against correctly rounded division (tests/test_gpu_numerics.py)
+extern "C" __global__ void dt_normalize_kernel(const double* __restrict__ in, double* __restrict__ out, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const V3 v = normalized(v3(in[3 * i], in[3 * i + 1], in[3 * i + 2]));
+  out[3 * i] = v.x;
+  out[3 * i + 1] = v.y;
+  out[3 * i + 2] = v.z;
+}
+
 // ---- host-side launch wrappers ---------------------------------------------------------
+extern "C" hipError_t dt_launch_normalize(const double* in, double* out, int64_t n, hipStream_t stream)
+{
+  hipLaunchKernelGGL(dt_normalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, in, out, n);
+  return hipGetLastError();
+}
 extern "C" size_t dt_launch_size(void) { return sizeof(DLaunch); }
 extern "C" size_t dt_scene_struct_offset(void) { return offsetof(DLaunch, S); }
 extern "C" size_t dt_params_struct_offset(void) { return offsetof(DLaunch, P); }

@@ -308,6 +308,9 @@ int dt_collect_stats(const dt_scene* s, void* stream, dt_stats* stats);
 
 /* diagnostic builds (-DDT_STAMPS): per-phase cycle sums of the last render; zeros otherwise */
 int dt_debug_counters(const dt_scene* s, uint64_t* out, int32_t n);
+/* numerics check: the device kernels' normalisation of n VEC3s (Eigen normalized(), dt_math.h),
+ * host arrays of 3n doubles; synchronous */
+int dt_debug_normalize(const double* in, double* out, int64_t n);
 
 /* renderImageCloud (render_final_project.cpp:1224-1279). Sets eye/up/lookingAt as the
  * reference does (1227-1229) on a local copy; g is not modified. */
