@@ -2189,6 +2189,9 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
         ocol[1][l] = ocol[1][l] + e.a.y;
         ocol[2][l] = ocol[2][l] + e.a.z;
       } else if (e.depth > 0) {
+#if DT_LAZY_ENTRY
+        pidx = sp;
+#endif
         have = true;
         break;
       }
