@@ -665,10 +665,14 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
     }
     hs.dn_pool = sc->d_dn_pool;
   }
-  // two items per queue atomic pays when every wave takes many items (C3: ~500, +2%); with few
-  // (C2: ~30) the coarser tail costs more (-11%)
+  // two items per queue atomic pays when every wave takes many items (C3: ~500, +2%; C3's 1/8
+  // tile share: 63, its kernel -3.3%, profiles/r03x); with few (C2: ~30) the coarser tail costs
+  // more (-11%). DT_BATCH_ITEMS: the items per wave from which DT_BATCH_SIZE (2) are dequeued at once
   dtd::DParams PL = P;
-  PL.item_batch = PL.n_items >= 64 * grid ? 2 : 1;
+  const char* bi = getenv("DT_BATCH_ITEMS");
+  const char* bs = getenv("DT_BATCH_SIZE");
+  const int64_t batch_from = bi && atoi(bi) > 0 ? atoi(bi) : 32;
+  PL.item_batch = PL.n_items >= batch_from * grid ? (bs && atoi(bs) > 0 ? atoi(bs) : 2) : 1;
   // deep-cascade waves raise their priority (dt_kernels.hip, DT_PRIO_STEPS) when the frame is split
   // over ranks, where one such wave bounds a rank's kernel; DT_PRIO_STEPS=<n> overrides (0: off)
   const char* ps = getenv("DT_PRIO_STEPS");
