@@ -1,9 +1,12 @@
 """Image-space tile split across ranks + gather of finished tiles.
 
-Every rank holds the whole (tiny) scene and renders one 32x32 tile of every group of `world`
+Every rank holds the whole (tiny) scene and renders one 8x8 tile of every group of `world`
 consecutive tiles (raster order), the ranks rotated by a hash of the group (dt_scene_dev.h
 tile_of), into a packed slab: the expensive sky/glossy regions spread over all GPUs, and unlike a
-plain t % world interleave no rank is tied to a fixed set of tile columns.
+plain t % world interleave no rank is tied to a fixed set of tile columns. 8x8 (the primary
+lists' block) rather than the ABI's default 32x32: sixteen times the tiles per rank even out the
+ranks' work (C3 at N=8: slowest rank 6.29 -> 5.96 ms, kernel-side bound 0.89 -> 0.94;
+profiles/r03z_rank_balance_tiles.log).
 The only exchange step is one gather of the finished slabs to rank 0 (torch.distributed:
 RCCL over xGMI on the GPU box, gloo in the CPU tests), after which rank 0 scatters the slabs
 into the ppmOut image (dt_unpack_slabs). Sample RNG is keyed on the global pixel index, so the
@@ -13,7 +16,7 @@ from . import DT_OUT_SLAB, slab_floats_max, tiles, unpack_slabs
 
 
 class FrameSplit:
-    def __init__(self, g, world, rank, tile_w=32, tile_h=32):
+    def __init__(self, g, world, rank, tile_w=8, tile_h=8):
         self.g = g
         self.world = world
         self.rank = rank

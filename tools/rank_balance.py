@@ -26,7 +26,8 @@ def main():
     for world in (1, 2, 4, 8):
         per, work = [], []
         for rank in (range(world) if not os.environ.get("REVERSE") else reversed(range(world))):
-            tile = dt.tiles(rank=rank, world=world, layout=dt.DT_OUT_SLAB)
+            ts = int(os.environ.get("TILE", "32"))   # tile side (FrameSplit: 32)
+            tile = dt.tiles(rank=rank, world=world, layout=dt.DT_OUT_SLAB, tile_w=ts, tile_h=ts)
             out = torch.zeros(max(dt.slab_floats(g, tile), 1), dtype=torch.float32, device="cuda")
             st = dt.render(scene, g, 240, out, tile)   # warm-up
             best = min(dt.render(scene, g, 240, out, tile).kernel_ms for _ in range(reps))
