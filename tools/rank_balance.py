@@ -4,7 +4,7 @@ trace-kernel time. With one GPU per rank the frame takes max_r T_r plus the gath
 T_1 / (N * max_r T_r) bounds the kernel-side strong-scaling efficiency of bench.py at N GPUs
 (load balance of the interleaved tiles, the persistent grid's tail on 1/N of the pixels).
 
-    python tools/rank_balance.py [c3|c2|c4] [reps]
+    python tools/rank_balance.py [c3|c2|c4] [reps]     (TILE=<side>: the split's tile side, default 8 as FrameSplit)
 """
 import json
 import os
@@ -26,7 +26,7 @@ def main():
     for world in (1, 2, 4, 8):
         per, work = [], []
         for rank in (range(world) if not os.environ.get("REVERSE") else reversed(range(world))):
-            ts = int(os.environ.get("TILE", "32"))   # tile side (FrameSplit: 32)
+            ts = int(os.environ.get("TILE", "8"))   # tile side (FrameSplit: 8)
             tile = dt.tiles(rank=rank, world=world, layout=dt.DT_OUT_SLAB, tile_w=ts, tile_h=ts)
             out = torch.zeros(max(dt.slab_floats(g, tile), 1), dtype=torch.float32, device="cuda")
             st = dt.render(scene, g, 240, out, tile)   # warm-up
