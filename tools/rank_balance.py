@@ -1,5 +1,5 @@
 """Per-rank share of the tile split on ONE GPU: for world N in {1, 2, 4, 8}, render every rank's
-slab (the tiles t % N == r, DT_OUT_SLAB) one after another on this device and report each rank's
+slab (its tiles of the hashed split, DT_OUT_SLAB) one after another on this device and report each rank's
 trace-kernel time. With one GPU per rank the frame takes max_r T_r plus the gather, so
 T_1 / (N * max_r T_r) bounds the kernel-side strong-scaling efficiency of bench.py at N GPUs
 (load balance of the interleaved tiles, the persistent grid's tail on 1/N of the pixels).
