@@ -765,16 +765,12 @@ int build_final(float frame, dt_globals& g, const std::string& data_dir, OwnedDe
   if (frame >= g.frame_cloud) {   // scene.h:788-803
     g.aperture = 0;
     g.antialias_samples = 1;
-    const double t = (frame - g.frame_cloud) / (double)(g.total - g.frame_cloud);
-    (void)t;
-    float tf = (frame - g.frame_cloud) / (float)(g.total - g.frame_cloud);
     V3 sunorange = v3(0.953, 0.51, 0.21), pastelpink = v3(1, 0.82, 0.863), violet = v3(0.541, 0.168, 0.886),
        indigo = v3(75.0 / 255, 0, 130.0 / 255), darkblue = v3(0.0667, 0.1137, 0.37);
     auto lerp = [&](double* c, V3 target) {
       V3 cur = v3a(c);
       set3(c, add(cur, divs(mul(frame - g.frame_cloud, sub(target, cur)), (g.total - g.frame_cloud))));
     };
-    (void)tf;
     lerp(g.redsky, sunorange);
     lerp(g.bluesky, pastelpink);
     lerp(g.sun_outer, violet);
