@@ -52,6 +52,7 @@
 // rectangle's plane must clear the hull by ypad more.
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -416,261 +417,319 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       }
     return all_in ? 1 : broken ? -1 : 0;
   };
-  std::vector<P3> umbra_q;   // the current light's points
-  // marks the umbra cells of light l: threads take rows of blocks (BX x BY x 1 cells); every cell
-  // tries the faces in the same order, so the result does not depend on the thread count
-  auto mark_umbra = [&](size_t l, std::vector<int32_t>& um) {
+  // Per light: the (leaf, cell) tests on bands of cell rows and the umbra marking on rows of
+  // blocks, then the lists packed into the pools. The tests and the umbra rows of every light run
+  // as one set of work items on one thread pool (threads pull items in light order); each item
+  // writes only its own rows of its light's arrays, every cell sees the leaves (faces) in the same
+  // order, so the lists and umbra cells are those of a one-thread build. The packing (identical
+  // lists stored once, across lights too) then runs light by light, as before.
+  struct LightSetup {
+    bool on = false;
+    double llo[3], lhi[3];
+    double lpts[5][3];
+    int n_lpts = 1;
+    std::vector<P3> lhull;   // hull culling and umbra cells (header): a point light; a rectangle's corners
+    double mud = 0;          // umbra margin
+    std::vector<int> fl;     // faces with the light strictly on one side
+  };
+  const size_t nl = std::min(lights.size(), (size_t)DT_MAX_SGRID);
+  std::vector<LightSetup> ls(nl);
+  for (size_t l = 0; l < nl; ++l) {
     const dtd::DLight& L = lights[l];
+    g.base[l] = -1;
+    if (L.type != DT_LIGHT_POINT && L.type != DT_LIGHT_RECT) continue;
+    LightSetup& S = ls[l];
+    S.on = true;
+    for (int a = 0; a < 3; ++a) {
+      if (L.type == DT_LIGHT_POINT) {
+        S.llo[a] = S.lhi[a] = L.center[a];
+      } else {   // parallelogram A, B, B + D - A, D (rect_sample stays inside it)
+        const double c = L.B[a] + L.D[a] - L.A[a];
+        S.llo[a] = std::min({L.A[a], L.B[a], L.D[a], c});
+        S.lhi[a] = std::max({L.A[a], L.B[a], L.D[a], c});
+      }
+      S.llo[a] -= m2;
+      S.lhi[a] += m2;
+    }
+    // light sample points for the list ordering: a point light, or a rectangle's centre and corners
+    for (int a = 0; a < 3; ++a) {
+      if (L.type == DT_LIGHT_POINT) {
+        S.lpts[0][a] = L.center[a];
+      } else {
+        S.lpts[0][a] = 0.5 * (L.B[a] + L.D[a]);
+        S.lpts[1][a] = L.A[a];
+        S.lpts[2][a] = L.B[a];
+        S.lpts[3][a] = L.D[a];
+        S.lpts[4][a] = L.B[a] + L.D[a] - L.A[a];
+      }
+    }
+    if (L.type != DT_LIGHT_POINT) S.n_lpts = 5;
+    if (L.type == DT_LIGHT_POINT) S.lhull.push_back({L.center[0], L.center[1], L.center[2]});
+    else
+      for (int k = 1; k < 5; ++k) S.lhull.push_back({S.lpts[k][0], S.lpts[k][1], S.lpts[k][2]});
+    if (!umbra_on) continue;
     // longest segment: from the grid box's far corner to the light (mu' keeps the leaf-box test)
     double lmax = 0;
     for (int k = 0; k < 8; ++k) {
       const P3 p = {lo[0] + ((k & 1) ? ext[0] : 0), lo[1] + ((k & 2) ? ext[1] : 0), lo[2] + ((k & 4) ? ext[2] : 0)};
-      for (const P3& q : umbra_q) lmax = std::max(lmax, std::sqrt(dot3(sub3(p, q), sub3(p, q))));
+      for (const P3& q : S.lhull) lmax = std::max(lmax, std::sqrt(dot3(sub3(p, q), sub3(p, q))));
     }
-    const double mud = std::max(mu, 2e-3 * (lmax + 1));
-    const int BX = std::max(1, blk_x), BY = std::max(1, blk_y);
-    const int nby = (g.dim[1] + BY - 1) / BY, nrows = nby * g.dim[2];
-    // faces with the light strictly on one side (the cells beyond may be in their umbra)
-    std::vector<int> fl;
+    S.mud = std::max(mu, 2e-3 * (lmax + 1));
     for (size_t fi = 0; fi < faces_all.size(); ++fi) {
       if (face_shape[fi] == L.shape_index) continue;   // skipped by the test (cpp:832)
       const Face& f = faces_all[fi];
       double qmn = INFINITY, qmx = -INFINITY;
-      for (const P3& q : umbra_q) {
+      for (const P3& q : S.lhull) {
         const double d = dot3(f.n, q) - f.c;
         qmn = std::min(qmn, d);
         qmx = std::max(qmx, d);
       }
-      if (qmn > mud || qmx < -mud) fl.push_back((int)fi);
+      if (qmn > S.mud || qmx < -S.mud) S.fl.push_back((int)fi);
     }
-    auto rows = [&](int t, int nt) {
-      for (int row = t; row < nrows; row += nt) {
-        const int z = row / nby, yb = (row % nby) * BY, ye = std::min(yb + BY, g.dim[1]) - 1;
-        for (int xb = 0; xb < g.dim[0]; xb += BX) {
-          const int xe = std::min(xb + BX, g.dim[0]) - 1;
-          double clo[3], chi[3];
-          const int c0[3] = {xb, yb, z}, c1[3] = {xe, ye, z};
-          for (int a = 0; a < 3; ++a) {
-            clo[a] = lo[a] + c0[a] * hh[a] - m1;
-            chi[a] = lo[a] + (c1[a] + 1) * hh[a] + m1;
-          }
-          for (int fi : fl) {
-            const Face& f = faces_all[fi];
-            const int32_t leaf = shape_leaf[face_shape[fi]];
-            const int r = box_umbra(f, clo, chi, umbra_q, mud);
-            if (r < 0) continue;
-            if (r == 0 && !umbra_cells_too) continue;
-            if (r > 0) {
-              for (int y = yb; y <= ye; ++y)
-                for (int x = xb; x <= xe; ++x) {
-                  int32_t& u = um[((size_t)z * g.dim[1] + y) * g.dim[0] + x];
-                  if (u < 0) u = leaf;
-                }
-              break;   // the whole block is settled
-            }
+  }
+  // umbra cells of light l, rows of blocks (BX x BY x 1 cells) t, t + nt, ...: every cell tries
+  // the faces in the same order, so the result does not depend on the partition
+  const int UBX = std::max(1, blk_x), UBY = std::max(1, blk_y);
+  const int unby = (g.dim[1] + UBY - 1) / UBY, unrows = unby * g.dim[2];
+  auto umbra_rows = [&](size_t l, std::vector<int32_t>& um, int t, int nt) {
+    const LightSetup& S = ls[l];
+    for (int row = t; row < unrows; row += nt) {
+      const int z = row / unby, yb = (row % unby) * UBY, ye = std::min(yb + UBY, g.dim[1]) - 1;
+      for (int xb = 0; xb < g.dim[0]; xb += UBX) {
+        const int xe = std::min(xb + UBX, g.dim[0]) - 1;
+        double clo[3], chi[3];
+        const int c0[3] = {xb, yb, z}, c1[3] = {xe, ye, z};
+        for (int a = 0; a < 3; ++a) {
+          clo[a] = lo[a] + c0[a] * hh[a] - m1;
+          chi[a] = lo[a] + (c1[a] + 1) * hh[a] + m1;
+        }
+        for (int fi : S.fl) {
+          const Face& f = faces_all[fi];
+          const int32_t leaf = shape_leaf[face_shape[fi]];
+          const int r = box_umbra(f, clo, chi, S.lhull, S.mud);
+          if (r < 0) continue;
+          if (r == 0 && !umbra_cells_too) continue;
+          if (r > 0) {
             for (int y = yb; y <= ye; ++y)
               for (int x = xb; x <= xe; ++x) {
                 int32_t& u = um[((size_t)z * g.dim[1] + y) * g.dim[0] + x];
-                if (u >= 0) continue;
-                const int cc[3] = {x, y, z};
-                double qlo[3], qhi[3];
-                for (int a = 0; a < 3; ++a) {
-                  qlo[a] = lo[a] + cc[a] * hh[a] - m1;
-                  qhi[a] = lo[a] + (cc[a] + 1) * hh[a] + m1;
-                }
-                if (box_umbra(f, qlo, qhi, umbra_q, mud) > 0) u = leaf;
+                if (u < 0) u = leaf;
               }
+            break;   // the whole block is settled
           }
+          for (int y = yb; y <= ye; ++y)
+            for (int x = xb; x <= xe; ++x) {
+              int32_t& u = um[((size_t)z * g.dim[1] + y) * g.dim[0] + x];
+              if (u >= 0) continue;
+              const int cc[3] = {x, y, z};
+              double qlo[3], qhi[3];
+              for (int a = 0; a < 3; ++a) {
+                qlo[a] = lo[a] + cc[a] * hh[a] - m1;
+                qhi[a] = lo[a] + (cc[a] + 1) * hh[a] + m1;
+              }
+              if (box_umbra(f, qlo, qhi, S.lhull, S.mud) > 0) u = leaf;
+            }
         }
       }
-    };
-    const int nt = std::max(1, std::min({hw_threads, nrows, 16}));
-    std::vector<std::thread> pool;
-    for (int t = 1; t < nt; ++t) pool.emplace_back(rows, t, nt);
-    rows(0, nt);
-    for (auto& th : pool) th.join();
+    }
   };
-  std::unordered_map<std::vector<int32_t>, uint32_t, VecHash> uniq;
-  std::vector<std::vector<int32_t>> lists(ncell);
-  const double t_setup = now_ms();
-  if (timing) fprintf(stderr, "  shadow grid setup: %.2f ms (%zu leaves, %d cells)\n", t_setup - t_entry, leaves.size(), ncell);
-  for (size_t l = 0; l < lights.size() && l < (size_t)DT_MAX_SGRID; ++l) {
+  // The (leaf, cell) tests of light l on the cell rows [row_lo, row_hi). Every band visits the
+  // leaves in the same order, so each cell's list comes out in leaf order, as from one thread.
+  const int rows = g.dim[1] * g.dim[2];
+  auto test_rows = [&](size_t l, std::vector<std::vector<int32_t>>& lists, int row_lo, int row_hi, long& dropped_n) {
     const dtd::DLight& L = lights[l];
-    g.base[l] = -1;
-    if (L.type != DT_LIGHT_POINT && L.type != DT_LIGHT_RECT) continue;
-    double llo[3], lhi[3];
-    for (int a = 0; a < 3; ++a) {
-      if (L.type == DT_LIGHT_POINT) {
-        llo[a] = lhi[a] = L.center[a];
-      } else {   // parallelogram A, B, B + D - A, D (rect_sample stays inside it)
-        const double c = L.B[a] + L.D[a] - L.A[a];
-        llo[a] = std::min({L.A[a], L.B[a], L.D[a], c});
-        lhi[a] = std::max({L.A[a], L.B[a], L.D[a], c});
-      }
-      llo[a] -= m2;
-      lhi[a] += m2;
-    }
-    // light sample points for the list ordering: a point light, or a rectangle's centre and corners
-    double lpts[5][3];
-    int n_lpts = 1;
-    for (int a = 0; a < 3; ++a) {
-      if (L.type == DT_LIGHT_POINT) {
-        lpts[0][a] = L.center[a];
-      } else {
-        lpts[0][a] = 0.5 * (L.B[a] + L.D[a]);
-        lpts[1][a] = L.A[a];
-        lpts[2][a] = L.B[a];
-        lpts[3][a] = L.D[a];
-        lpts[4][a] = L.B[a] + L.D[a] - L.A[a];
-      }
-    }
-    if (L.type != DT_LIGHT_POINT) n_lpts = 5;
-    // hull culling and umbra cells (header): the light's points (a point light; a rectangle's corners)
-    std::vector<P3> lhull;
-    if (L.type == DT_LIGHT_POINT) lhull.push_back({L.center[0], L.center[1], L.center[2]});
-    else
-      for (int k = 1; k < 5; ++k) lhull.push_back({lpts[k][0], lpts[k][1], lpts[k][2]});
-    umbra_q = lhull;
-    const double t_light = now_ms();
-    for (auto& v : lists) v.clear();
-    // The (leaf, cell) tests run on worker threads, each owning a band of (z, y) cell rows. Every
-    // thread visits the leaves in the same order, so each cell's list comes out in leaf order, as
-    // from one thread.
-    const int rows = g.dim[1] * g.dim[2];
-    const int nthr = std::max(1, std::min({hw_threads, rows, 16}));
-    std::vector<long> dropped_t(nthr, 0);
-    auto work = [&](int t) {
-      const int row_lo = (int)((long)rows * t / nthr), row_hi = (int)((long)rows * (t + 1) / nthr);
-      std::vector<int> shp;
-      std::vector<P3> shull, hA(8 + lhull.size());
-      for (size_t k = 0; k < lhull.size(); ++k) hA[8 + k] = lhull[k];
-      for (int leaf : leaves) {
-        const dtd::DNodeDev& nd = nodes[leaf];
-        // the light's own shape is skipped by the shadow test (cpp:832): a leaf holding only it
-        // never occludes this light
-        if ((nd.meta & dtd::DN_SINGLE) && (int32_t)nd.first == L.shape_index) continue;
-        const double* blo = lbox[leaf].data();
-        const double* bhi = lbox[leaf].data() + 3;
-        int r0[3], r1[3];
-        for (int a = 0; a < 3; ++a) cell_range(lo[a], hh[a], g.dim[a], m1, llo[a], lhi[a], blo[a], bhi[a], r0[a], r1[a]);
-        if (r0[0] > r1[0]) continue;
-        bool have_shapes = false;
-        // Cells go in blocks of BX x BY x 1. A cell's box lies inside its block's box, so when the
-        // block's swept box misses the leaf box, or all the leaf's shapes are separated from the
-        // block, the same holds for every cell in it. The lists come out as from per-cell tests
-        // (the margins m1 and mplane lie far above the rounding of the box corners).
-        const int BX = blk_x, BY = blk_y;
-        bool have_hull = false;   // shull: the leaf's hull points (empty: a shape without one)
-        P3 hint = {0, 0, 0};      // last GJK direction for this leaf (neighbouring cells separate alike)
-        auto separated = [&](const double* clo, const double* chi, int hmode) {
-          bool sep = !shp.empty();
+    const LightSetup& S = ls[l];
+    const double* llo = S.llo;
+    const double* lhi = S.lhi;
+    const std::vector<P3>& lhull = S.lhull;
+    std::vector<int> shp;
+    std::vector<P3> shull, hA(8 + lhull.size());
+    for (size_t k = 0; k < lhull.size(); ++k) hA[8 + k] = lhull[k];
+    for (int leaf : leaves) {
+      const dtd::DNodeDev& nd = nodes[leaf];
+      // the light's own shape is skipped by the shadow test (cpp:832): a leaf holding only it
+      // never occludes this light
+      if ((nd.meta & dtd::DN_SINGLE) && (int32_t)nd.first == L.shape_index) continue;
+      const double* blo = lbox[leaf].data();
+      const double* bhi = lbox[leaf].data() + 3;
+      int r0[3], r1[3];
+      for (int a = 0; a < 3; ++a) cell_range(lo[a], hh[a], g.dim[a], m1, llo[a], lhi[a], blo[a], bhi[a], r0[a], r1[a]);
+      if (r0[0] > r1[0]) continue;
+      bool have_shapes = false;
+      // Cells go in blocks of BX x BY x 1. A cell's box lies inside its block's box, so when the
+      // block's swept box misses the leaf box, or all the leaf's shapes are separated from the
+      // block, the same holds for every cell in it. The lists come out as from per-cell tests
+      // (the margins m1 and mplane lie far above the rounding of the box corners).
+      const int BX = blk_x, BY = blk_y;
+      bool have_hull = false;   // shull: the leaf's hull points (empty: a shape without one)
+      P3 hint = {0, 0, 0};      // last GJK direction for this leaf (neighbouring cells separate alike)
+      auto separated = [&](const double* clo, const double* chi, int hmode) {
+        bool sep = !shp.empty();
+        for (int sid : shp)
+          if (sid != L.shape_index &&
+              !shape_separated(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, clo, chi, llo, lhi, mplane, ypad)) {
+            sep = false;
+            break;
+          }
+        if (sep || hull_cull < hmode) return sep;
+        if (!have_hull) {
+          have_hull = true;
+          shull.clear();
           for (int sid : shp)
             if (sid != L.shape_index &&
-                !shape_separated(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, clo, chi, llo, lhi, mplane, ypad)) {
-              sep = false;
+                !shape_hull_points(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, ypad, shull, up_only)) {
+              shull.clear();
               break;
             }
-          if (sep || hull_cull < hmode) return sep;
-          if (!have_hull) {
-            have_hull = true;
-            shull.clear();
-            for (int sid : shp)
-              if (sid != L.shape_index &&
-                  !shape_hull_points(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, ypad, shull, up_only)) {
-                shull.clear();
-                break;
-              }
-          }
-          if (shull.empty()) return false;
-          for (int k = 0; k < 8; ++k) hA[k] = {(k & 1) ? chi[0] : clo[0], (k & 2) ? chi[1] : clo[1], (k & 4) ? chi[2] : clo[2]};
-          return hulls_separated(hA.data(), (int)hA.size(), shull.data(), (int)shull.size(), m2 + mplane, hint);
-        };
-        auto cell_box = [&](int x0, int y0, int z0, int x1, int y1, int z1, double* clo, double* chi) {
-          const int c0[3] = {x0, y0, z0}, c1[3] = {x1, y1, z1};
-          for (int a = 0; a < 3; ++a) {
-            clo[a] = lo[a] + c0[a] * hh[a] - m1;
-            chi[a] = lo[a] + (c1[a] + 1) * hh[a] + m1;
-          }
-        };
-        for (int z = r0[2]; z <= r1[2]; ++z)
-          for (int yb = r0[1]; yb <= r1[1]; yb += BY) {
-            const int ye = std::min(yb + BY - 1, r1[1]);
-            if (z * g.dim[1] + ye < row_lo || z * g.dim[1] + yb >= row_hi) continue;
-            if (!have_shapes) { leaf_shapes(leaf, shp); have_shapes = true; }
-            for (int xb = r0[0]; xb <= r1[0]; xb += BX) {
-              const int xe = std::min(xb + BX - 1, r1[0]);
-              double clo[3], chi[3];
-              cell_box(xb, yb, z, xe, ye, z, clo, chi);
-              if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
-              const bool block_sep = separated(clo, chi, 1);
-              for (int y = yb; y <= ye; ++y) {
-                const int row = z * g.dim[1] + y;
-                if (row < row_lo || row >= row_hi) continue;
-                for (int x = xb; x <= xe; ++x) {
-                  cell_box(x, y, z, x, y, z, clo, chi);
-                  if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
-                  if (block_sep || separated(clo, chi, 2)) { ++dropped_t[t]; continue; }
-                  lists[(size_t)row * g.dim[0] + x].push_back(leaf);
-                }
+        }
+        if (shull.empty()) return false;
+        for (int k = 0; k < 8; ++k) hA[k] = {(k & 1) ? chi[0] : clo[0], (k & 2) ? chi[1] : clo[1], (k & 4) ? chi[2] : clo[2]};
+        return hulls_separated(hA.data(), (int)hA.size(), shull.data(), (int)shull.size(), m2 + mplane, hint);
+      };
+      auto cell_box = [&](int x0, int y0, int z0, int x1, int y1, int z1, double* clo, double* chi) {
+        const int c0[3] = {x0, y0, z0}, c1[3] = {x1, y1, z1};
+        for (int a = 0; a < 3; ++a) {
+          clo[a] = lo[a] + c0[a] * hh[a] - m1;
+          chi[a] = lo[a] + (c1[a] + 1) * hh[a] + m1;
+        }
+      };
+      for (int z = r0[2]; z <= r1[2]; ++z)
+        for (int yb = r0[1]; yb <= r1[1]; yb += BY) {
+          const int ye = std::min(yb + BY - 1, r1[1]);
+          if (z * g.dim[1] + ye < row_lo || z * g.dim[1] + yb >= row_hi) continue;
+          if (!have_shapes) { leaf_shapes(leaf, shp); have_shapes = true; }
+          for (int xb = r0[0]; xb <= r1[0]; xb += BX) {
+            const int xe = std::min(xb + BX - 1, r1[0]);
+            double clo[3], chi[3];
+            cell_box(xb, yb, z, xe, ye, z, clo, chi);
+            if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
+            const bool block_sep = separated(clo, chi, 1);
+            for (int y = yb; y <= ye; ++y) {
+              const int row = z * g.dim[1] + y;
+              if (row < row_lo || row >= row_hi) continue;
+              for (int x = xb; x <= xe; ++x) {
+                cell_box(x, y, z, x, y, z, clo, chi);
+                if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
+                if (block_sep || separated(clo, chi, 2)) { ++dropped_n; continue; }
+                lists[(size_t)row * g.dim[0] + x].push_back(leaf);
               }
             }
           }
+        }
+    }
+    // Likely occluders first. The test is any-hit, so the order never changes an answer, but a
+    // lane stops testing at its first occluder and a wave leaves the list once all its lanes
+    // are occluded. Score: how many segments from the cell centre to the light's sample points
+    // (centre and corners) cross the leaf box; ties keep leaf order.
+    if (!order_lists) return;
+    std::vector<std::pair<int, int32_t>> keyed;
+    for (int row = row_lo; row < row_hi; ++row) {
+      const int y = row % g.dim[1], z = row / g.dim[1];
+      for (int x = 0; x < g.dim[0]; ++x) {
+        std::vector<int32_t>& v = lists[(size_t)row * g.dim[0] + x];
+        if (v.size() < 2 || (int)v.size() > max_list) continue;
+        const int ci[3] = {x, y, z};
+        double p[3];
+        for (int a = 0; a < 3; ++a) p[a] = lo[a] + (ci[a] + 0.5) * hh[a];
+        keyed.clear();
+        for (int32_t leaf : v) {
+          int sc = 0;
+          for (int k = 0; k < S.n_lpts; ++k) sc += segment_meets_box(p, S.lpts[k], lbox[leaf].data(), lbox[leaf].data() + 3);
+          keyed.push_back({-sc, leaf});
+        }
+        std::stable_sort(keyed.begin(), keyed.end(),
+                         [](const std::pair<int, int32_t>& a, const std::pair<int, int32_t>& b) { return a.first < b.first; });
+        for (size_t k = 0; k < v.size(); ++k) v[k] = keyed[k].second;
       }
-      // Likely occluders first. The test is any-hit, so the order never changes an answer, but a
-      // lane stops testing at its first occluder and a wave leaves the list once all its lanes
-      // are occluded. Score: how many segments from the cell centre to the light's sample points
-      // (centre and corners) cross the leaf box; ties keep leaf order.
-      if (!order_lists) return;
-      std::vector<std::pair<int, int32_t>> keyed;
-      for (int row = row_lo; row < row_hi; ++row) {
-        const int y = row % g.dim[1], z = row / g.dim[1];
-        for (int x = 0; x < g.dim[0]; ++x) {
-          std::vector<int32_t>& v = lists[(size_t)row * g.dim[0] + x];
-          if (v.size() < 2 || (int)v.size() > max_list) continue;
-          const int ci[3] = {x, y, z};
-          double p[3];
-          for (int a = 0; a < 3; ++a) p[a] = lo[a] + (ci[a] + 0.5) * hh[a];
-          keyed.clear();
-          for (int32_t leaf : v) {
-            int s = 0;
-            for (int k = 0; k < n_lpts; ++k) s += segment_meets_box(p, lpts[k], lbox[leaf].data(), lbox[leaf].data() + 3);
-            keyed.push_back({-s, leaf});
-          }
-          std::stable_sort(keyed.begin(), keyed.end(),
-                           [](const std::pair<int, int32_t>& a, const std::pair<int, int32_t>& b) { return a.first < b.first; });
-          for (size_t k = 0; k < v.size(); ++k) v[k] = keyed[k].second;
+    }
+  };
+  std::vector<std::vector<std::vector<int32_t>>> lists_l(nl);
+  std::vector<std::vector<int32_t>> umbra_l(nl);   // per cell: the occluding face's leaf, or -1
+  struct Item { int l, kind, t, nt; };             // kind 0: test rows, 1: umbra rows
+  std::vector<Item> items;
+  const int nthr = std::max(1, std::min({hw_threads, rows, 16}));
+  const int nt_u = std::max(1, std::min({hw_threads, unrows, 16}));
+  for (size_t l = 0; l < nl; ++l) {
+    if (!ls[l].on) continue;
+    lists_l[l].resize(ncell);
+    umbra_l[l].assign(ncell, -1);
+    for (int t = 0; t < nthr; ++t) items.push_back({(int)l, 0, t, nthr});
+    if (umbra_on)
+      for (int t = 0; t < nt_u; ++t) items.push_back({(int)l, 1, t, nt_u});
+  }
+  std::vector<long> dropped_item(items.size(), 0);
+  const double t_setup = now_ms();
+  if (timing) fprintf(stderr, "  shadow grid setup: %.2f ms (%zu leaves, %d cells)\n", t_setup - t_entry, leaves.size(), ncell);
+  {
+    std::atomic<size_t> next(0);
+    auto runner = [&]() {
+      for (size_t k; (k = next.fetch_add(1)) < items.size();) {
+        const Item& it = items[k];
+        if (it.kind == 0)
+          test_rows((size_t)it.l, lists_l[it.l], (int)((long)rows * it.t / it.nt), (int)((long)rows * (it.t + 1) / it.nt),
+                    dropped_item[k]);
+        else
+          umbra_rows((size_t)it.l, umbra_l[it.l], it.t, it.nt);
+      }
+    };
+    const int np = std::max(1, std::min(hw_threads, 16));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < np; ++t) pool.emplace_back(runner);
+    runner();
+    for (auto& th : pool) th.join();
+  }
+  for (long d : dropped_item) dropped += d;
+  const double t_tests = now_ms();
+  // umbra cells keep their face's leaf alone; every list hashed on the pool too
+  std::vector<std::vector<uint64_t>> hash_l(nl);
+  {
+    std::atomic<size_t> next(0);
+    auto runner = [&]() {
+      for (size_t l; (l = next.fetch_add(1)) < nl;) {
+        if (!ls[l].on) continue;
+        hash_l[l].resize(ncell);
+        for (int c = 0; c < ncell; ++c) {
+          std::vector<int32_t>& v = lists_l[l][c];
+          if (umbra_l[l][c] >= 0) v.assign(1, umbra_l[l][c]);
+          hash_l[l][c] = VecHash()(v);
         }
       }
     };
     std::vector<std::thread> pool;
-    for (int t = 1; t < nthr; ++t) pool.emplace_back(work, t);
-    work(0);
+    for (size_t t = 1; t < std::min(nl, (size_t)std::max(1, std::min(hw_threads, 16))); ++t) pool.emplace_back(runner);
+    runner();
     for (auto& th : pool) th.join();
-    for (long d : dropped_t) dropped += d;
-    std::vector<int32_t> umbra(ncell, -1);   // the occluding face's leaf
-    const double t_umbra = now_ms();
-    if (umbra_on) mark_umbra(l, umbra);
-    const double t_tests = now_ms();
+  }
+  // identical lists are stored once, in first-occurrence order over lights then cells (the pools
+  // do not depend on the thread count): hash -> (offset, length), contents compared on a match
+  std::unordered_multimap<uint64_t, std::pair<uint32_t, uint32_t>> seen;
+  seen.reserve((size_t)ncell);
+  for (size_t l = 0; l < nl; ++l) {
+    if (!ls[l].on) continue;
+    std::vector<std::vector<int32_t>>& lists = lists_l[l];
+    const std::vector<int32_t>& umbra = umbra_l[l];
     g.base[l] = (int32_t)g.cells.size() / 2;
     for (int c = 0; c < ncell; ++c) {
-      std::vector<int32_t>& v = lists[c];
-      if (umbra[c] >= 0) {
-        v.assign(1, umbra[c]);
-        ++g.umbra_cells;
-      }
+      const std::vector<int32_t>& v = lists[c];
+      if (umbra[c] >= 0) ++g.umbra_cells;
       if ((int)v.size() > max_list) {   // the tree walk is cheaper for long lists
         g.cells.push_back(0);
         g.cells.push_back(DT_SG_WALK);
         continue;
       }
-      auto it = uniq.find(v);
-      uint32_t off;
-      if (it == uniq.end()) {
+      uint32_t off = 0;
+      bool found = false;
+      auto range = seen.equal_range(hash_l[l][c]);
+      for (auto it = range.first; it != range.second && !found; ++it)
+        if (it->second.second == (uint32_t)v.size() &&
+            std::equal(v.begin(), v.end(), g.list.begin() + it->second.first)) {
+          off = it->second.first;
+          found = true;
+        }
+      if (!found) {
         off = (uint32_t)g.list.size();
         g.list.insert(g.list.end(), v.begin(), v.end());
-        uniq.emplace(v, off);
-      } else {
-        off = it->second;
+        seen.emplace(hash_l[l][c], std::make_pair(off, (uint32_t)v.size()));
       }
       g.cells.push_back(off | (umbra[c] >= 0 ? DT_SG_UMBRA : 0u));
       g.cells.push_back((uint32_t)v.size());
@@ -686,10 +745,10 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       fprintf(stderr, "  shadow grid light %zu: union of cell lists %zu of %zu leaves, %zu tree cells\n", l, nu,
               leaves.size(), tree_cells);
     }
-    if (timing)
-      fprintf(stderr, "  shadow grid light %zu: tests %.2f ms (%d threads), umbra %.2f ms, lists %.2f ms\n", l,
-              t_umbra - t_light, nthr, t_tests - t_umbra, now_ms() - t_tests);
   }
+  if (timing)
+    fprintf(stderr, "  shadow grid: tests and umbra of %zu lights %.2f ms (%d threads), lists %.2f ms\n", nl,
+            t_tests - t_setup, std::max(1, std::min(hw_threads, 16)), now_ms() - t_tests);
   g.plane_dropped = dropped;
   if (timing) fprintf(stderr, "  shadow grid lights: %.2f ms\n", now_ms() - t_setup);
   return g.n_lights > 0;
