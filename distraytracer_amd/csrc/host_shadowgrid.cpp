@@ -58,7 +58,6 @@
 #include <cstdlib>
 #include <cmath>
 #include <thread>
-#include <unordered_map>
 #include <vector>
 
 #include "host_internal.h"
@@ -320,15 +319,6 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   auto now_ms = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const int hw_threads = (int)std::max(1u, std::thread::hardware_concurrency());
 
-  // identical lists are stored once (cells of one light, and across lights)
-  struct VecHash {
-    size_t operator()(const std::vector<int32_t>& v) const
-    {
-      uint64_t h = 1469598103934665603ull ^ v.size();
-      for (int32_t x : v) h = (h ^ (uint32_t)x) * 1099511628211ull;
-      return (size_t)h;
-    }
-  };
   // umbra cells (header), DT_SG_UMBRA: 0 off, 1 whole blocks of cells (default), 2 also single
   // cells of the other blocks (C3: 2.7% more umbra cells for 4x the host time)
   const char* su = getenv("DT_SG_UMBRA");
@@ -536,7 +526,13 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   // The (leaf, cell) tests of light l on the cell rows [row_lo, row_hi). Every band visits the
   // leaves in the same order, so each cell's list comes out in leaf order, as from one thread.
   const int rows = g.dim[1] * g.dim[2];
-  auto test_rows = [&](size_t l, std::vector<std::vector<int32_t>>& lists, int row_lo, int row_hi, long& dropped_n) {
+  // a band's lists, CSR: cells [cell_lo, cell_hi), cell c's leaves ent[off[c - cell_lo], off[c - cell_lo + 1])
+  struct Band {
+    int cell_lo = 0, cell_hi = 0;
+    std::vector<int32_t> off, ent;
+  };
+  auto test_rows = [&](size_t l, Band& band, int row_lo, int row_hi, long& dropped_n) {
+    std::vector<std::pair<int32_t, int32_t>> pr;   // (cell, leaf), each cell's leaves in leaf order
     const dtd::DLight& L = lights[l];
     const LightSetup& S = ls[l];
     const double* llo = S.llo;
@@ -611,11 +607,22 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
                 cell_box(x, y, z, x, y, z, clo, chi);
                 if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
                 if (block_sep || separated(clo, chi, 2)) { ++dropped_n; continue; }
-                lists[(size_t)row * g.dim[0] + x].push_back(leaf);
+                pr.push_back({(int32_t)((size_t)row * g.dim[0] + x), leaf});
               }
             }
           }
         }
+    }
+    // stable counting sort by cell: each cell's leaves keep their (leaf) order
+    band.cell_lo = (int)((size_t)row_lo * g.dim[0]);
+    band.cell_hi = (int)((size_t)row_hi * g.dim[0]);
+    band.off.assign((size_t)(band.cell_hi - band.cell_lo) + 1, 0);
+    for (const auto& e : pr) ++band.off[(size_t)(e.first - band.cell_lo) + 1];
+    for (size_t k = 1; k < band.off.size(); ++k) band.off[k] += band.off[k - 1];
+    band.ent.resize(pr.size());
+    {
+      std::vector<int32_t> pos(band.off.begin(), band.off.end() - 1);
+      for (const auto& e : pr) band.ent[(size_t)pos[(size_t)(e.first - band.cell_lo)]++] = e.second;
     }
     // Likely occluders first. The test is any-hit, so the order never changes an answer, but a
     // lane stops testing at its first occluder and a wave leaves the list once all its lanes
@@ -626,24 +633,27 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
     for (int row = row_lo; row < row_hi; ++row) {
       const int y = row % g.dim[1], z = row / g.dim[1];
       for (int x = 0; x < g.dim[0]; ++x) {
-        std::vector<int32_t>& v = lists[(size_t)row * g.dim[0] + x];
-        if (v.size() < 2 || (int)v.size() > max_list) continue;
+        const size_t ci_ = (size_t)row * g.dim[0] + x - (size_t)band.cell_lo;
+        int32_t* v = band.ent.data() + band.off[ci_];
+        const int n = band.off[ci_ + 1] - band.off[ci_];
+        if (n < 2 || n > max_list) continue;
         const int ci[3] = {x, y, z};
         double p[3];
         for (int a = 0; a < 3; ++a) p[a] = lo[a] + (ci[a] + 0.5) * hh[a];
         keyed.clear();
-        for (int32_t leaf : v) {
+        for (int k2 = 0; k2 < n; ++k2) {
+          const int32_t leaf = v[k2];
           int sc = 0;
           for (int k = 0; k < S.n_lpts; ++k) sc += segment_meets_box(p, S.lpts[k], lbox[leaf].data(), lbox[leaf].data() + 3);
           keyed.push_back({-sc, leaf});
         }
         std::stable_sort(keyed.begin(), keyed.end(),
                          [](const std::pair<int, int32_t>& a, const std::pair<int, int32_t>& b) { return a.first < b.first; });
-        for (size_t k = 0; k < v.size(); ++k) v[k] = keyed[k].second;
+        for (int k = 0; k < n; ++k) v[k] = keyed[(size_t)k].second;
       }
     }
   };
-  std::vector<std::vector<std::vector<int32_t>>> lists_l(nl);
+  std::vector<std::vector<Band>> bands_l(nl);
   std::vector<std::vector<int32_t>> umbra_l(nl);   // per cell: the occluding face's leaf, or -1
   struct Item { int l, kind, t, nt; };             // kind 0: test rows, 1: umbra rows
   std::vector<Item> items;
@@ -651,7 +661,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   const int nt_u = std::max(1, std::min({hw_threads, unrows, 16}));
   for (size_t l = 0; l < nl; ++l) {
     if (!ls[l].on) continue;
-    lists_l[l].resize(ncell);
+    bands_l[l].resize((size_t)nthr);
     umbra_l[l].assign(ncell, -1);
     for (int t = 0; t < nthr; ++t) items.push_back({(int)l, 0, t, nthr});
     if (umbra_on)
@@ -666,8 +676,8 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       for (size_t k; (k = next.fetch_add(1)) < items.size();) {
         const Item& it = items[k];
         if (it.kind == 0)
-          test_rows((size_t)it.l, lists_l[it.l], (int)((long)rows * it.t / it.nt), (int)((long)rows * (it.t + 1) / it.nt),
-                    dropped_item[k]);
+          test_rows((size_t)it.l, bands_l[it.l][(size_t)it.t], (int)((long)rows * it.t / it.nt),
+                    (int)((long)rows * (it.t + 1) / it.nt), dropped_item[k]);
         else
           umbra_rows((size_t)it.l, umbra_l[it.l], it.t, it.nt);
       }
@@ -680,71 +690,77 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   }
   for (long d : dropped_item) dropped += d;
   const double t_tests = now_ms();
-  // umbra cells keep their face's leaf alone; every list hashed on the pool too
-  std::vector<std::vector<uint64_t>> hash_l(nl);
-  {
-    std::atomic<size_t> next(0);
-    auto runner = [&]() {
-      for (size_t l; (l = next.fetch_add(1)) < nl;) {
-        if (!ls[l].on) continue;
-        hash_l[l].resize(ncell);
-        for (int c = 0; c < ncell; ++c) {
-          std::vector<int32_t>& v = lists_l[l][c];
-          if (umbra_l[l][c] >= 0) v.assign(1, umbra_l[l][c]);
-          hash_l[l][c] = VecHash()(v);
-        }
-      }
-    };
-    std::vector<std::thread> pool;
-    for (size_t t = 1; t < std::min(nl, (size_t)std::max(1, std::min(hw_threads, 16))); ++t) pool.emplace_back(runner);
-    runner();
-    for (auto& th : pool) th.join();
-  }
   // identical lists are stored once, in first-occurrence order over lights then cells (the pools
-  // do not depend on the thread count): hash -> (offset, length), contents compared on a match
-  std::unordered_multimap<uint64_t, std::pair<uint32_t, uint32_t>> seen;
-  seen.reserve((size_t)ncell);
+  // do not depend on the thread count): hash -> (offset, length), contents compared on a match.
+  // An umbra cell's list is its face's leaf alone.
+  // open addressing: slot = (hash, offset, length); a length of 0xffffffff marks an empty slot
+  struct Seen { uint64_t h; uint32_t off, len; };
+  std::vector<Seen> seen((size_t)1 << 16, Seen{0, 0, 0xffffffffu});
+  size_t n_seen = 0;
+  auto seen_insert = [&](std::vector<Seen>& tab, const Seen& e) {
+    size_t k = (size_t)(e.h ^ (e.h >> 29)) & (tab.size() - 1);
+    while (tab[k].len != 0xffffffffu) k = (k + 1) & (tab.size() - 1);
+    tab[k] = e;
+  };
+  g.cells.reserve(g.cells.size() + 2 * (size_t)ncell * nl);
   for (size_t l = 0; l < nl; ++l) {
     if (!ls[l].on) continue;
-    std::vector<std::vector<int32_t>>& lists = lists_l[l];
     const std::vector<int32_t>& umbra = umbra_l[l];
     g.base[l] = (int32_t)g.cells.size() / 2;
+    size_t b = 0;
+    std::vector<char> in_union;
+    size_t nu = 0, tree_cells = 0;
+    const bool verbose = getenv("DT_SG_VERBOSE") != nullptr;
+    if (verbose) in_union.assign(nodes.size(), 0);
     for (int c = 0; c < ncell; ++c) {
-      const std::vector<int32_t>& v = lists[c];
-      if (umbra[c] >= 0) ++g.umbra_cells;
-      if ((int)v.size() > max_list) {   // the tree walk is cheaper for long lists
+      while (c >= bands_l[l][b].cell_hi) ++b;
+      const Band& band = bands_l[l][b];
+      const size_t ci = (size_t)(c - band.cell_lo);
+      const int32_t* v = band.ent.data() + band.off[ci];
+      int n = band.off[ci + 1] - band.off[ci];
+      if (umbra[c] >= 0) {
+        v = &umbra[c];
+        n = 1;
+        ++g.umbra_cells;
+      }
+      if (verbose) {
+        if (n > max_list) ++tree_cells;
+        for (int k = 0; k < n; ++k) if (!in_union[v[k]]) { in_union[v[k]] = 1; ++nu; }
+      }
+      if (n > max_list) {   // the tree walk is cheaper for long lists
         g.cells.push_back(0);
         g.cells.push_back(DT_SG_WALK);
         continue;
       }
+      uint64_t h = 1469598103934665603ull ^ (uint64_t)n;
+      for (int k = 0; k < n; ++k) h = (h ^ (uint32_t)v[k]) * 1099511628211ull;
       uint32_t off = 0;
       bool found = false;
-      auto range = seen.equal_range(hash_l[l][c]);
-      for (auto it = range.first; it != range.second && !found; ++it)
-        if (it->second.second == (uint32_t)v.size() &&
-            std::equal(v.begin(), v.end(), g.list.begin() + it->second.first)) {
-          off = it->second.first;
+      for (size_t k = (size_t)(h ^ (h >> 29)) & (seen.size() - 1); seen[k].len != 0xffffffffu; k = (k + 1) & (seen.size() - 1))
+        if (seen[k].h == h && seen[k].len == (uint32_t)n && std::equal(v, v + n, g.list.begin() + seen[k].off)) {
+          off = seen[k].off;
           found = true;
+          break;
         }
       if (!found) {
         off = (uint32_t)g.list.size();
-        g.list.insert(g.list.end(), v.begin(), v.end());
-        seen.emplace(hash_l[l][c], std::make_pair(off, (uint32_t)v.size()));
+        g.list.insert(g.list.end(), v, v + n);
+        if (2 * (n_seen + 1) > seen.size()) {   // keep the load under 1/2
+          std::vector<Seen> bigger(seen.size() * 2, Seen{0, 0, 0xffffffffu});
+          for (const Seen& e : seen)
+            if (e.len != 0xffffffffu) seen_insert(bigger, e);
+          seen.swap(bigger);
+        }
+        seen_insert(seen, Seen{h, off, (uint32_t)n});
+        ++n_seen;
       }
       g.cells.push_back(off | (umbra[c] >= 0 ? DT_SG_UMBRA : 0u));
-      g.cells.push_back((uint32_t)v.size());
+      g.cells.push_back((uint32_t)n);
     }
     g.n_lights = (int)l + 1;
-    if (getenv("DT_SG_VERBOSE")) {
-      std::vector<char> in_union(nodes.size(), 0);
-      size_t nu = 0, tree_cells = 0;
-      for (int c = 0; c < ncell; ++c) {
-        if ((int)lists[c].size() > max_list) ++tree_cells;
-        for (int32_t x : lists[c]) if (!in_union[x]) { in_union[x] = 1; ++nu; }
-      }
+    if (verbose)
       fprintf(stderr, "  shadow grid light %zu: union of cell lists %zu of %zu leaves, %zu tree cells\n", l, nu,
               leaves.size(), tree_cells);
-    }
   }
   if (timing)
     fprintf(stderr, "  shadow grid: tests and umbra of %zu lights %.2f ms (%d threads), lists %.2f ms\n", nl,
