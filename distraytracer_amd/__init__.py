@@ -146,6 +146,34 @@ def collect_stats(scene, stream=None):
     return st
 
 
+def _ptr_typed(a, torch_dtype, np_dtype):
+    if hasattr(a, "data_ptr"):
+        if str(a.dtype) != torch_dtype or not a.is_contiguous():
+            raise DTError("expected a contiguous %s tensor" % torch_dtype)
+        return ctypes.c_void_p(a.data_ptr()), 1 if a.is_cuda else 0
+    import numpy as np
+    if a.dtype != np.dtype(np_dtype) or not a.flags["C_CONTIGUOUS"]:
+        raise DTError("expected a contiguous %s array" % np_dtype)
+    return ctypes.c_void_p(a.ctypes.data), 0
+
+
+def intersect_primary(scene, g, frame, first_ray, hit_shape, hit_t, stream=None):
+    """The intersection micro-benchmark: closest hit of primary rays first_ray ..
+    first_ray + len(hit_shape) - 1 of the globals' camera (include/dt.h dt_intersect_primary).
+    hit_shape: int32, hit_t: float32, both host or both device. Returns the kernel's ms."""
+    sp, sdev = _ptr_typed(hit_shape, "torch.int32", "int32")
+    tp, tdev = _ptr_typed(hit_t, "torch.float32", "float32")
+    n = hit_shape.numel() if hasattr(hit_shape, "numel") else hit_shape.size
+    nt = hit_t.numel() if hasattr(hit_t, "numel") else hit_t.size
+    if sdev != tdev or n != nt:
+        raise DTError("hit_shape and hit_t: same length, same side")
+    ms = ctypes.c_float(0)
+    check(lib.dt_intersect_primary(scene.handle, ctypes.byref(g), int(frame), int(first_ray), int(n), sp, tp, sdev,
+                                   ctypes.c_void_p(stream) if stream else None, ctypes.byref(ms)),
+          "dt_intersect_primary")
+    return ms.value
+
+
 def render_sky(g, frame, out, tile=None, stream=None):
     """renderImageCloud's pixel loop (sky only) into `out`."""
     st = Stats()

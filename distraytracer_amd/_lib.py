@@ -117,7 +117,7 @@ EXPORTS = ["dt_abi_version", "dt_last_error", "dt_globals_default", "dt_scene_cr
            "dt_scene_bvh", "dt_bvh_build", "dt_accel_info_build", "dt_slab_floats", "dt_slab_floats_max",
            "dt_render", "dt_render_async", "dt_collect_stats", "dt_debug_counters", "dt_render_sky",
            "dt_unpack_slabs", "dt_build_scene", "dt_scene_desc_free", "dt_write_ppm", "dt_write_png",
-           "dt_mocap_bone_table", "dt_debug_normalize"]
+           "dt_mocap_bone_table", "dt_debug_normalize", "dt_intersect_primary"]
 
 
 class DTError(RuntimeError):
@@ -171,6 +171,8 @@ def _load():
         "dt_debug_normalize": (c_int32, [P(c_double), P(c_double), c_int64]),
         "dt_render_sky": (c_int32, [P(Globals), c_float, P(Tiles), ctypes.c_void_p, c_int32, ctypes.c_void_p,
                                     P(Stats)]),
+        "dt_intersect_primary": (c_int32, [ctypes.c_void_p, P(Globals), c_int32, c_int64, c_int64, ctypes.c_void_p,
+                                           ctypes.c_void_p, c_int32, ctypes.c_void_p, P(c_float)]),
         "dt_unpack_slabs": (c_int32, [P(Globals), P(Tiles), c_int32, ctypes.c_void_p, ctypes.c_void_p, c_int32,
                                       ctypes.c_void_p]),
         "dt_build_scene": (c_int32, [ctypes.c_char_p, c_float, P(Globals), ctypes.c_char_p, P(P(SceneDesc))]),

@@ -30,6 +30,9 @@ extern "C" const void* dt_trace_kernel_rpc_ptr(void);
 extern "C" hipError_t dt_launch_trace_dn(const void* dev_launch, float* out, int grid, hipStream_t stream);
 extern "C" hipError_t dt_launch_normalize(const double* in, double* out, int64_t n, hipStream_t stream);
 extern "C" const void* dt_trace_kernel_dn_ptr(void);
+extern "C" hipError_t dt_launch_isect(const void* dev_launch, int64_t first, int64_t n, int32_t* hit_shape, float* hit_t,
+                                      int grid, hipStream_t stream);
+extern "C" const void* dt_isect_kernel_ptr(void);
 
 namespace {
 
@@ -603,6 +606,26 @@ static int upload_primary_lists(dt_scene* sc)
   return DT_OK;
 }
 
+// the device pointers of a scene's uploaded structures, as the kernels' DScene sees them
+static void fill_hscene(const dt_scene* sc, HScene& hs)
+{
+  memset(&hs, 0, sizeof(hs));
+  hs.nodes = sc->d_nodes;
+  hs.fnodes = sc->d_fnodes;
+  hs.bnodes = sc->d_bnodes;
+  hs.bparent = (const int32_t*)sc->d_bparent;
+  hs.sg_cells = (const uint32_t*)sc->d_sg_cells;
+  hs.sg_list = (const int32_t*)sc->d_sg_list;
+  hs.leaf_idx = (const int32_t*)sc->d_leaf;
+  hs.hdr = sc->d_hdr;
+  hs.geom = (const double*)sc->d_geom;
+  hs.mat = sc->d_mat;
+  hs.lights = sc->d_lights;
+  hs.tex = (const uint8_t*)sc->d_tex;
+  hs.pl_cells = (const uint32_t*)sc->d_pl_cells;
+  hs.pl_list = (const uint32_t*)sc->d_pl_list;
+}
+
 static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>& zs, float* out_dev,
                           hipStream_t st)
 {
@@ -622,23 +645,10 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   }
   if (nz) memcpy(sc->h_zs, zs.data(), nz * sizeof(float));
   HScene hs;
-  hs.nodes = sc->d_nodes;
-  hs.fnodes = sc->d_fnodes;
-  hs.bnodes = sc->d_bnodes;
-  hs.bparent = (const int32_t*)sc->d_bparent;
-  hs.sg_cells = (const uint32_t*)sc->d_sg_cells;
-  hs.sg_list = (const int32_t*)sc->d_sg_list;
-  hs.leaf_idx = (const int32_t*)sc->d_leaf;
-  hs.hdr = sc->d_hdr;
-  hs.geom = (const double*)sc->d_geom;
-  hs.mat = sc->d_mat;
-  hs.lights = sc->d_lights;
-  hs.tex = (const uint8_t*)sc->d_tex;
+  fill_hscene(sc, hs);
   hs.cloud_z = (const float*)sc->d_zs;
   hs.stats = sc->d_stats;
   hs.queue = sc->d_stats + ST_N;
-  hs.pl_cells = (const uint32_t*)sc->d_pl_cells;
-  hs.pl_list = (const uint32_t*)sc->d_pl_list;
   // scenes with a RectPrismWithCylinder take the trace kernel compiled with its tests (dt_kernels.hip
   // DT_WITH_RPC), whose occupancy may differ. DFS work sharing inside the wave (dt_trace_kernel_dn)
   // when DT_DONATE=1; its pre-order paths hold 10 levels of 3 bits (max_depth <= 11, brdf_samples <= 6)
@@ -816,6 +826,82 @@ int dt_render(const dt_scene* sc_c, const dt_globals* g, int32_t frame, const dt
   if (rc == DT_OK) rc = dt_collect_stats(sc, stream, stats);
   if (!out_on_device) (void)hipFree(dout);
   return rc;
+}
+
+// Intersection micro-benchmark: dt_isect_kernel over rays first_ray .. first_ray+n_rays-1
+// of the globals' camera. Synchronous; its own launch record and counters, so it may run beside
+// renders of the same scene on other streams.
+int dt_intersect_primary(const dt_scene* sc_c, const dt_globals* g, int32_t frame, int64_t first_ray, int64_t n_rays,
+                         int32_t* hit_shape, float* hit_t, int32_t out_on_device, void* stream, float* kernel_ms)
+{
+  dt_scene* sc = const_cast<dt_scene*>(sc_c);
+  if (!sc || !g || !hit_shape || !hit_t) return fail(DT_E_INVALID, "null argument");
+  if (first_ray < 0 || n_rays < 0) return fail(DT_E_INVALID, "negative ray range");
+  if (sc->no_cull) return fail(DT_E_UNSUPPORTED, "dt_intersect_primary: scenes with a RectPrismWithCylinder");
+  if (n_rays == 0) {
+    if (kernel_ms) *kernel_ms = 0;
+    return DT_OK;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  dtd::DParams P;
+  std::vector<float> zs;
+  dt_tiles whole;
+  memset(&whole, 0, sizeof(whole));
+  whole.world = 1;
+  int rc = prepare_render(sc, g, frame, &whole, P, zs);
+  if (rc) return rc;
+  if ((rc = scene_upload(sc)) || (rc = update_primary_lists(sc, P, true))) return rc;
+  struct Tmp {   // released on every return path
+    void *launch = nullptr, *stats = nullptr, *shape = nullptr, *t = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    ~Tmp()
+    {
+      for (void* b : {launch, stats, shape, t})
+        if (b) (void)hipFree(b);
+      if (e0) (void)hipEventDestroy(e0);
+      if (e1) (void)hipEventDestroy(e1);
+    }
+  } tmp;
+  const size_t n_stats = sizeof(unsigned long long) * (ST_N + 1);
+  HIPCHK(hipMalloc(&tmp.launch, dt_launch_size()));
+  HIPCHK(hipMalloc(&tmp.stats, n_stats));
+  HIPCHK(hipMemsetAsync(tmp.stats, 0, n_stats, st));
+  HScene hs;
+  fill_hscene(sc, hs);
+  hs.stats = (unsigned long long*)tmp.stats;
+  hs.queue = hs.stats + ST_N;
+  std::vector<uint8_t> L(dt_launch_size(), 0);
+  memcpy(L.data() + dt_scene_struct_offset(), &hs, sizeof(hs));
+  memcpy(L.data() + dt_params_struct_offset(), &P, sizeof(P));
+  HIPCHK(hipMemcpyAsync(tmp.launch, L.data(), L.size(), hipMemcpyHostToDevice, st));
+  int32_t* dshape = hit_shape;
+  float* dt_ = hit_t;
+  if (!out_on_device) {
+    HIPCHK(hipMalloc(&tmp.shape, (size_t)n_rays * sizeof(int32_t)));
+    HIPCHK(hipMalloc(&tmp.t, (size_t)n_rays * sizeof(float)));
+    dshape = (int32_t*)tmp.shape;
+    dt_ = (float*)tmp.t;
+  }
+  static int resident = 0;
+  if (!resident) resident = max_resident_waves(dt_isect_kernel_ptr(), 64);
+  const int64_t waves = (n_rays + 63) / 64;
+  const int grid = (int)(waves < resident ? waves : resident);
+  HIPCHK(hipEventCreate(&tmp.e0));
+  HIPCHK(hipEventCreate(&tmp.e1));
+  HIPCHK(hipEventRecord(tmp.e0, st));
+  HIPCHK(dt_launch_isect(tmp.launch, first_ray, n_rays, dshape, dt_, grid > 0 ? grid : 1, st));
+  HIPCHK(hipEventRecord(tmp.e1, st));
+  if (!out_on_device) {
+    HIPCHK(hipMemcpyAsync(hit_shape, dshape, (size_t)n_rays * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(hit_t, dt_, (size_t)n_rays * sizeof(float), hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  if (kernel_ms) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, tmp.e0, tmp.e1));
+    *kernel_ms = ms;
+  }
+  return DT_OK;
 }
 
 int dt_render_sky(const dt_globals* g, float frame, const dt_tiles* tiles, float* out, int32_t out_on_device,

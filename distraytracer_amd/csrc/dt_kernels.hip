@@ -73,6 +73,12 @@ using namespace dtd;
 #ifndef DT_DONATE
 #define DT_DONATE 0
 #endif
+// DT_ISECT=1 (a fourth compilation, build/dt_kernels_isect.o): only dt_isect_kernel, the intersection
+// micro-benchmark, so that its call sites of the shared device functions stay out of the trace kernel's
+// object
+#ifndef DT_ISECT
+#define DT_ISECT 0
+#endif
 #if DT_WITH_RPC
 #define DT_TRACE_KERNEL dt_trace_kernel_rpc
 #elif DT_DONATE
@@ -2724,6 +2730,71 @@ struct DLaunch {
 #ifndef DT_TRACE_MIN_WAVES
 #define DT_TRACE_MIN_WAVES 1
 #endif
+#if DT_ISECT
+// Intersection micro-benchmark (2^24 primary rays of the C3 camera): rayColor's first
+// step for the camera's primary rays (getDOFSamples + getPerspEyeRay, cpp:195-210 / 1044-1072; the
+// BVH gather and closest hit, cpp:491-538), taken exactly as the trace kernel takes it for a root
+// ray -- the pixel block's primary list when the wave's rays share a block, else the fast tree --
+// one ray per lane. Ray r (pixel-major, DT_ISECT_RPP rays per pixel): q = r / RPP, pixel q mod W*H
+// (raster order), sample r mod RPP + RPP * (q div W*H). Out: the hit shape (-1: none) and its t
+// (FLT_MAX: none), as oracle/oracle.c or_primary_hit.
+#define DT_ISECT_RPP 8
+extern "C" __global__ void __launch_bounds__(64)
+dt_isect_kernel(const DLaunch* __restrict__ Lp, int64_t first, int64_t n, int32_t* __restrict__ hit_shape,
+                float* __restrict__ hit_t)
+{
+  const DScene& S = Lp->S;
+  const DParams& P = Lp->P;
+  const int lane = threadIdx.x;
+  __shared__ unsigned int wc_lds[WC_N];
+  if (lane < WC_N) wc_lds[lane] = 0;
+  __syncthreads();
+  Counters cnt;
+  cnt.wc = wc_lds;
+  cnt.box = 0; cnt.prim = 0; cnt.wnodes = 0;
+  Ctx c;
+  c.S = &S;
+  c.P = &P;
+  c.rng.k0 = P.seed;
+  c.rng.k1 = (uint32_t)P.frame;
+  const int64_t npx = (int64_t)P.xRes * P.yRes;
+  const bool lists = P.pl_block > 0 && P.n_fnodes > 0 && (P.ftree_mode & 1);
+  for (int64_t base = (int64_t)blockIdx.x * DT_WAVE; base < n; base += (int64_t)gridDim.x * DT_WAVE) {
+    const int64_t i = base + lane;
+    const bool act = i < n;
+    const int64_t r = first + i;
+    const int64_t q = r / DT_ISECT_RPP;
+    const int64_t p = q % npx;
+    const int x = (int)(p % P.xRes), y = (int)(p / P.xRes);
+    c.rng.pixel = (uint32_t)(y * P.xRes + x);
+    c.rng.sample = (uint32_t)(r % DT_ISECT_RPP + DT_ISECT_RPP * (q / npx));
+    V3 eye_sample = v3a(P.eye), ray0 = v3(0, 0, 0);
+    if (act) camera_ray(c, P, x, y, eye_sample, ray0);
+    int pblock = -1;
+    if (lists) {
+      const int blk = (y / P.pl_block) * P.pl_nbx + x / P.pl_block;
+      const int b0 = uni(blk);
+      if (!__ballot(act && blk != b0)) pblock = b0;
+    }
+    HitRec h;
+    const bool any = closest_hit(S, P, act, ray0, eye_sample, 0.0f, h, cnt, pblock);
+    if (act) {
+      const bool hit = any && h.shape >= 0;
+      hit_shape[i] = hit ? h.shape : -1;
+      hit_t[i] = hit ? h.t_min : FLT_MAX;
+    }
+  }
+  if (lane == 0) atomicAdd(S.stats + ST_WNODES, (unsigned long long)cnt.wnodes);
+}
+extern "C" hipError_t dt_launch_isect(const void* dev_launch, int64_t first, int64_t n, int32_t* hit_shape, float* hit_t,
+                                      int grid, hipStream_t stream)
+{
+  hipLaunchKernelGGL(dt_isect_kernel, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, first, n, hit_shape,
+                     hit_t);
+  return hipGetLastError();
+}
+extern "C" const void* dt_isect_kernel_ptr(void) { return (const void*)dt_isect_kernel; }
+#else
 extern "C" __global__ void __launch_bounds__(64, DT_TRACE_MIN_WAVES)
 DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
 {
@@ -2963,7 +3034,9 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   }
 }
 
-#if !DT_WITH_RPC && !DT_DONATE
+#endif   // !DT_ISECT
+
+#if !DT_WITH_RPC && !DT_DONATE && !DT_ISECT
 // The sky of the pixels a 1-spp trace launch flagged as missed (P.sky_defer): renderImage's miss
 // branch (cpp:1074-1092: cloudColor of mcam * focalPoint) one pixel per lane, at the occupancy of a
 // small kernel instead of inside the trace kernel's register budget. With one sample the pixel is
@@ -3105,6 +3178,7 @@ extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_
   return hipGetLastError();
 }
 extern "C" const void* dt_trace_kernel_ptr(void) { return (const void*)dt_trace_kernel; }
+#elif DT_ISECT
 #elif DT_DONATE   // the trace kernel with DFS work sharing inside the wave
 extern "C" hipError_t dt_launch_trace_dn(const void* dev_launch, float* out, int grid, hipStream_t stream)
 {

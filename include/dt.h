@@ -312,6 +312,17 @@ int dt_debug_counters(const dt_scene* s, uint64_t* out, int32_t n);
  * host arrays of 3n doubles; synchronous */
 int dt_debug_normalize(const double* in, double* out, int64_t n);
 
+/* Intersection micro-benchmark (2^24 primary rays of the C3 camera). rayColor's first
+ * step (render_final_project.cpp:491-538: BVH gather + closest hit) for primary rays of the globals'
+ * camera (getDOFSamples + getPerspEyeRay, 195-210 / 1044-1072), as dt_render takes it. Ray r:
+ * q = r / 8 -> pixel q mod (xRes*yRes) in raster order, sample r mod 8 + 8 * (q div (xRes*yRes)).
+ * hit_shape[i], hit_t[i] for ray first_ray + i: the closest shape (-1: none) and its t (FLT_MAX:
+ * none); host (out_on_device=0) or device (1) arrays of n_rays. Synchronous; kernel_ms (optional):
+ * the kernel's HIP-event time. Scenes with a RectPrismWithCylinder: DT_E_UNSUPPORTED. */
+int dt_intersect_primary(const dt_scene* s, const dt_globals* g, int32_t frame, int64_t first_ray,
+                         int64_t n_rays, int32_t* hit_shape, float* hit_t, int32_t out_on_device,
+                         void* stream, float* kernel_ms);
+
 /* renderImageCloud (render_final_project.cpp:1224-1279). Sets eye/up/lookingAt as the
  * reference does (1227-1229) on a local copy; g is not modified. */
 int dt_render_sky(const dt_globals* g, float frame, const dt_tiles* tiles, float* out,

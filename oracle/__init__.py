@@ -48,6 +48,9 @@ def oracle():
         o.or_render_work.restype = ctypes.c_int
         o.or_render_work.argtypes = [P(SceneDesc), P(Globals), ctypes.c_int, P(Tiles), ctypes.c_void_p, ctypes.c_int,
                                      P(Stats), P(ctypes.c_uint64)]
+        o.or_primary_hit.restype = ctypes.c_int
+        o.or_primary_hit.argtypes = [P(SceneDesc), P(Globals), ctypes.c_int, ctypes.c_longlong, ctypes.c_longlong,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         o.or_sample_color.restype = ctypes.c_int
         o.or_sample_color.argtypes = [P(SceneDesc), P(Globals), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, P(ctypes.c_double), P(ctypes.c_int)]
@@ -128,3 +131,16 @@ def sample_color(desc, g, frame, x, y, sample):
     if rc:
         raise RuntimeError("or_sample_color failed %d" % rc)
     return list(col), bool(hit.value)
+
+
+def primary_hit(desc, g, frame, first, n, nthreads=0):
+    """closest hits of the intersection micro-benchmark's rays first .. first+n-1 (or_primary_hit):
+    (shape int32[n], t float32[n])"""
+    import numpy as np
+    shape = np.empty(n, dtype=np.int32)
+    t = np.empty(n, dtype=np.float32)
+    rc = oracle().or_primary_hit(_desc_ptr(desc), ctypes.byref(g), int(frame), int(first), int(n),
+                                 ctypes.c_void_p(shape.ctypes.data), ctypes.c_void_p(t.ctypes.data), int(nthreads))
+    if rc:
+        raise RuntimeError("or_primary_hit failed %d" % rc)
+    return shape, t

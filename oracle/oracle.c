@@ -1958,6 +1958,74 @@ int or_sample_color(const dt_scene_desc* d, const dt_globals* g, int frame, int 
   return rc;
 }
 
+/* The intersection micro-benchmark's reference (include/dt.h dt_intersect_primary): for primary rays
+ * first .. first+n-1 (ray r: q = r / 8, pixel q mod W*H, sample r mod 8 + 8 (q div W*H)), the
+ * camera ray of render_sample (getDOFSamples + getPerspEyeRay, cpp:195-210, 1062-1072) and
+ * rayColor's gather + closest hit (cpp:491-538, ray_color above): the closest shape (-1: none)
+ * and its t (FLT_MAX: none). */
+int or_primary_hit(const dt_scene_desc* d, const dt_globals* g, int frame, long long first, long long n,
+                   int* shape, float* t, int nthreads)
+{
+  RenderCtx R;
+  int rc = render_setup(&R, d, g, frame);
+  if (rc != DT_OK) { scene_free(&R.scene); return rc; }
+  const long long npx = (long long)g->xRes * g->yRes;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+#endif
+  {
+    int* inds = (int*)malloc(sizeof(int) * (d->n_shapes > 0 ? d->n_shapes : 1));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 256)
+#endif
+    for (long long i = 0; i < n; ++i) {
+      const long long r = first + i, q = r / 8, p = q % npx;
+      const int x = (int)(p % g->xRes), y = (int)(p / g->xRes);
+      const Cam* cam = &R.cam;
+      Ctx c;
+      c.s = &R.scene;
+      c.st = NULL;
+      c.wk = NULL;
+      c.shift = 0.0f;
+      c.rng.key[0] = g->seed;
+      c.rng.key[1] = (uint32_t)frame;
+      c.rng.pixel = (uint32_t)(y * g->xRes + x);
+      c.rng.sample = (uint32_t)(r % 8 + 8 * (q / npx));
+      V3 eye_sample = cam->eye;
+      if (g->aperture > 0) {
+        double u0, u1;
+        rng2(&c.rng, 0, P_DOF, 0, &u0, &u1);
+        float rr = (float)(g->aperture / 2 * u0);
+        float theta = (float)(2 * M_PI * u1);
+        eye_sample = add(add(cam->eye, mul(rr * cr_cosf(theta), cam->X)), mul(rr * cr_sinf(theta), cam->Y));
+      }
+      V3 focalPoint = add(cam->eye, mul(g->focal_length, persp_eye_ray(g, cam, x, y)));
+      V3 ray = sub(focalPoint, eye_sample);
+      int n_inds = bvh_gather(&c, ray, eye_sample, inds);
+      float t_dist = FLT_MAX, t_min = FLT_MAX;
+      int any = 0, hit_i = -1;
+      for (int k = 0; k < n_inds; ++k) {
+        int ins = 0, hole = -1;
+        V3 hc;
+        if (shape_intersect(&c, inds[k], ray, eye_sample, &t_dist, &ins, &hc, &hole)) {
+          any = 1;
+          if (t_dist < t_min) {
+            hit_i = inds[k];
+            t_min = t_dist;
+          }
+        }
+      }
+      const int hit = any && hit_i >= 0;
+      shape[i] = hit ? hit_i : -1;
+      t[i] = hit ? t_min : FLT_MAX;
+    }
+    free(inds);
+  }
+  scene_free(&R.scene);
+  return DT_OK;
+}
+
 int or_render_work(const dt_scene_desc* d, const dt_globals* g, int frame, const dt_tiles* tiles, float* out,
                    int nthreads, dt_stats* stats, uint64_t* work);
 

@@ -61,6 +61,10 @@ int or_render(const dt_scene_desc* d, const dt_globals* g, int frame, const dt_t
 int or_render_work(const dt_scene_desc* d, const dt_globals* g, int frame, const dt_tiles* tiles,
                    float* out, int nthreads, dt_stats* stats, uint64_t* work);
 
+/* the intersection micro-benchmark's closest hits (include/dt.h dt_intersect_primary numbering) */
+int or_primary_hit(const dt_scene_desc* d, const dt_globals* g, int frame, long long first, long long n,
+                   int* shape, float* t, int nthreads);
+
 /* one rayColor call tree for a single pixel-sample (debug / unit tests) */
 int or_sample_color(const dt_scene_desc* d, const dt_globals* g, int frame, int x, int y,
                     int sample, double out_color[3], int* out_hit);

@@ -361,3 +361,27 @@ def test_work_header_and_oracle_counts():
     assert n["light"] == st.shadow_rays and n["hit"] <= st.rays and n["box"] > 0
     assert n["sky"] >= st.sky_pixels   # the reference loop marches once per missing sample
     assert work.price(wk) == pytest.approx(sum(float(c) * w for c, w in zip(wk, work.WEIGHTS)))
+
+
+def test_oracle_primary_hit_numbering():
+    """or_primary_hit (the intersection micro-benchmark's reference) follows dt_intersect_primary's
+    ray numbering and the render's camera: a ray hits iff the same pixel-sample's rayColor tree in
+    or_sample_color reports a hit (the root step decides it: no hit, no children); and the closest hit
+    is the first of the ray's gathered shapes in distance, t > 0."""
+    g, b = final240()
+    g.xRes, g.yRes = 64, 48
+    npx = g.xRes * g.yRes
+    rays = [0, 7, 8, 1000, 8 * npx - 1, 8 * npx, 8 * npx + 13, 3 * 8 * npx + 5]
+    for r in rays:
+        shape, t = oracle.primary_hit(b, g, 240, r, 1)
+        q = r // 8
+        p = q % npx
+        x, y, s = p % g.xRes, p // g.xRes, r % 8 + 8 * (q // npx)
+        _, hit = oracle.sample_color(b, g, 240, x, y, s)
+        assert (shape[0] >= 0) == hit, r
+        assert (t[0] > 0 and t[0] < 3.4e38) if hit else t[0] == np.float32(3.4028235e38)
+    # a window equals the concatenation of its halves (per-ray results, any thread count)
+    s1, t1 = oracle.primary_hit(b, g, 240, 100, 512, nthreads=4)
+    s2, t2 = oracle.primary_hit(b, g, 240, 100, 256, nthreads=1)
+    s3, t3 = oracle.primary_hit(b, g, 240, 356, 256, nthreads=2)
+    assert np.array_equal(s1, np.concatenate([s2, s3])) and np.array_equal(t1, np.concatenate([t2, t3]))

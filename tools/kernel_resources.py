@@ -46,7 +46,8 @@ if __name__ == "__main__":
     build = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "distraytracer_amd", "csrc", "build")
     ap.add_argument("objects", nargs="*", default=[os.path.join(build, "dt_kernels.o"),
                                                    os.path.join(build, "dt_kernels_rpc.o"),
-                                                   os.path.join(build, "dt_kernels_dn.o")])
+                                                   os.path.join(build, "dt_kernels_dn.o"),
+                                                   os.path.join(build, "dt_kernels_isect.o")])
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     r = {}
