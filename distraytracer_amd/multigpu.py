@@ -47,21 +47,47 @@ class FrameSplit:
 class GatherPipeline:
     """Double-buffered frame gather: frame k renders into slab k%2; submit(k) starts its gather
     (async collective) and first completes frame k-1's (wait + scatter into the image on rank
-    0), so one frame's gather runs beside the next frame's render. finish() drains."""
+    0), so one frame's gather runs beside the next frame's render. finish() drains.
 
-    def __init__(self, split, slabs, gathered, image):
+    streams (optional, two torch.cuda.Streams): frame k renders on streams[k%2] (call begin(k)
+    first, and render with a scene object of its own per stream: a scene's launches share one
+    launch record), so frame k+1's waves start on the CUs frame k's last waves leave idle. The
+    collective and the scatter stay on torch's current stream, ordered after the render by an
+    event; a slab is rendered into again only after its gather and scatter (ev_free). Without
+    streams, frames render on the current stream."""
+
+    def __init__(self, split, slabs, gathered, image, streams=None):
         self.split = split
         self.slabs = slabs          # two per-rank slab buffers
         self.gathered = gathered    # two world*slab_floats buffers on rank 0 (ignored elsewhere)
         self.image = image
+        self.streams = streams
+        self.ev_free = [None, None]
         self.pending = None
 
     def slab(self, k):
         return self.slabs[k % 2]
 
+    def stream(self, k):
+        """the stream frame k renders on (None: torch's current stream)"""
+        return self.streams[k % 2] if self.streams else None
+
+    def begin(self, k):
+        """before frame k's render: its stream waits until slab k%2's previous gather is done"""
+        if self.streams and self.ev_free[k % 2] is not None:
+            self.streams[k % 2].wait_event(self.ev_free[k % 2])
+
     def submit(self, k):
-        self.finish()
         b = k % 2
+        rendered = None
+        if self.streams:
+            import torch
+            rendered = torch.cuda.Event()
+            rendered.record(self.streams[b])
+        self.finish()
+        if rendered is not None:
+            import torch
+            torch.cuda.current_stream(self.slabs[b].device).wait_event(rendered)
         work = self.split.gather(self.slabs[b], self.gathered[b] if self.split.rank == 0 else None, async_op=True)
         self.pending = (work, b)
 
@@ -70,9 +96,15 @@ class GatherPipeline:
             return
         work, b = self.pending
         self.pending = None
-        work.wait()   # orders torch's current stream after the collective
+        if work is not None:
+            work.wait()   # orders torch's current stream after the collective
         if self.split.rank == 0:
             self.split.assemble(self.gathered[b], self.image)   # on that same stream
+        if self.streams:
+            import torch
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.slabs[b].device))
+            self.ev_free[b] = ev
 
 
 class FrameQueue:

@@ -112,6 +112,51 @@ def test_gather_pipeline_over_rccl(cuda):
         dist.destroy_process_group()
 
 
+def test_gather_pipeline_two_streams_over_rccl(cuda):
+    """bench.py's N > 1 path with two frames in flight (its default): frame k renders on
+    streams[k % 2] with a scene object of its own, GatherPipeline orders the gather after the render
+    by an event and the next render into a slab after that slab's gather. Every assembled image
+    equals a plain full-frame render of its frame."""
+    import torch.distributed as dist
+    from distraytracer_amd.multigpu import FrameSplit, GatherPipeline
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        g = dt.globals_default()
+        g.use_model = 0
+        built = dt.build_scene("final", 240, g)
+        g.xRes, g.yRes, g.antialias_samples, g.max_depth = 240, 136, 4, 3
+        scenes = [dt.Scene(built, g), dt.Scene(built, g)]
+        split = FrameSplit(g, 1, 0)
+        dev = torch.device("cuda", 0)
+        z = lambda n: torch.zeros(n, dtype=torch.float32, device=dev)
+        streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        pipe = GatherPipeline(split, [z(split.slab_floats), z(split.slab_floats)],
+                              [z(split.slab_floats), z(split.slab_floats)], z(3 * g.xRes * g.yRes), streams=streams)
+        images = []
+        n = 5
+        for k in range(n):
+            g.seed = k
+            pipe.begin(k)
+            dt.render_async(scenes[k % 2], g, 240, pipe.slab(k), split.tile, stream=pipe.stream(k).cuda_stream)
+            pipe.submit(k)   # completes frame k-1 into the image
+            if k > 0:
+                images.append(pipe.image.clone())
+        pipe.finish()
+        images.append(pipe.image.clone())
+        torch.cuda.synchronize()
+        assert len(images) == n
+        for k, img in enumerate(images):
+            g.seed = k
+            ref = z(3 * g.xRes * g.yRes)
+            dt.render(scenes[0], g, 240, ref, dt.tiles())
+            assert torch.equal(img, ref), k
+        for sc in scenes:
+            sc.close()
+    finally:
+        dist.destroy_process_group()
+
+
 def test_negative_blur_shift_at_render_time(cuda):
     """The bump tree and the blur-padded shadow-grid lists of a tunnel frame are padded for
     non-negative shifts only (the build globals' move_per_frame, accel_t >= 0: host_accel.cpp
