@@ -851,17 +851,20 @@ int dt_intersect_primary(const dt_scene* sc_c, const dt_globals* g, int32_t fram
   int rc = prepare_render(sc, g, frame, &whole, P, zs);
   if (rc) return rc;
   if ((rc = scene_upload(sc)) || (rc = update_primary_lists(sc, P, true))) return rc;
-  struct Tmp {   // released on every return path
+  struct Tmp {   // released on every return path, after the stream's work that may use them
+    hipStream_t st = nullptr;
     void *launch = nullptr, *stats = nullptr, *shape = nullptr, *t = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     ~Tmp()
     {
+      if (launch) (void)hipStreamSynchronize(st);
       for (void* b : {launch, stats, shape, t})
         if (b) (void)hipFree(b);
       if (e0) (void)hipEventDestroy(e0);
       if (e1) (void)hipEventDestroy(e1);
     }
   } tmp;
+  tmp.st = st;
   const size_t n_stats = sizeof(unsigned long long) * (ST_N + 1);
   HIPCHK(hipMalloc(&tmp.launch, dt_launch_size()));
   HIPCHK(hipMalloc(&tmp.stats, n_stats));
