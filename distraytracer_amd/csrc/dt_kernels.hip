@@ -209,6 +209,31 @@ __device__ __forceinline__ double pw_rt(double x, double y)
 {
   if (y >= 0 && y <= 64 && y == (double)(int)y) {
     int n = (int)y;
+#if DT_PHONG_DD
+    // double-double binary powering (exact products by fma): the rounded result matches glibc's
+    // pow for 99.9% of x instead of 21%
+    double rh = 1.0, rl = 0.0, bh = x, bl = 0.0;
+    while (n) {
+      if (n & 1) {
+        const double p = rh * bh;
+        double e = __builtin_fma(rh, bh, -p);
+        e = e + (rh * bl + rl * bh);
+        const double s = p + e;
+        rl = e - (s - p);
+        rh = s;
+      }
+      n >>= 1;
+      if (n) {
+        const double p = bh * bh;
+        double e = __builtin_fma(bh, bh, -p);
+        e = e + 2.0 * (bh * bl);
+        const double s = p + e;
+        bl = e - (s - p);
+        bh = s;
+      }
+    }
+    return rh + rl;
+#else
     double r = 1.0, b = x;
     while (n) {
       if (n & 1) r = r * b;
@@ -216,6 +241,7 @@ __device__ __forceinline__ double pw_rt(double x, double y)
       if (n) b = b * b;
     }
     return r;
+#endif
   }
   return pow(x, y);
 }
