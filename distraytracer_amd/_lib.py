@@ -117,7 +117,8 @@ EXPORTS = ["dt_abi_version", "dt_last_error", "dt_globals_default", "dt_scene_cr
            "dt_scene_bvh", "dt_bvh_build", "dt_accel_info_build", "dt_slab_floats", "dt_slab_floats_max",
            "dt_render", "dt_render_async", "dt_collect_stats", "dt_debug_counters", "dt_render_sky",
            "dt_unpack_slabs", "dt_build_scene", "dt_scene_desc_free", "dt_write_ppm", "dt_write_png",
-           "dt_mocap_bone_table", "dt_debug_normalize", "dt_intersect_primary"]
+           "dt_mocap_bone_table", "dt_debug_normalize", "dt_intersect_primary",
+           "dt_debug_load_obj"]
 
 
 class DTError(RuntimeError):
@@ -177,6 +178,8 @@ def _load():
                                       ctypes.c_void_p]),
         "dt_build_scene": (c_int32, [ctypes.c_char_p, c_float, P(Globals), ctypes.c_char_p, P(P(SceneDesc))]),
         "dt_scene_desc_free": (None, [P(SceneDesc)]),
+        "dt_debug_load_obj": (c_int32, [ctypes.c_char_p, ctypes.c_void_p, c_int64, ctypes.c_void_p, c_int64,
+                                        ctypes.c_void_p, c_int64, P(c_int64)]),
         "dt_write_ppm": (c_int32, [ctypes.c_char_p, c_int32, c_int32, ctypes.c_void_p]),
         "dt_write_png": (c_int32, [ctypes.c_char_p, c_int32, c_int32, ctypes.c_void_p]),
         "dt_mocap_bone_table": (c_int32, [ctypes.c_char_p, ctypes.c_char_p, P(c_int32), c_int32,

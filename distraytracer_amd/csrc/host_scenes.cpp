@@ -969,3 +969,41 @@ extern "C" void dt_scene_desc_free(dt_scene_desc* d)
 {
   if (d) delete reinterpret_cast<OwnedDesc*>(d);
 }
+
+// the OBJ ingest as finalBuildModels sees it (load_obj above, objHelper.h:6-85): counts, then the
+// vertices and texcoords as the floats tinyobj's real_t holds and 6 ints per triangle (vertex and
+// texcoord indices, 0-based, texcoord -1 when absent). tests/test_oracle_obj.py compares it with
+// the reference's own vendored tiny_obj_loader.h (oracle/ref/obj_parse.cpp).
+extern "C" int dt_debug_load_obj(const char* path, float* v, int64_t cap_v, float* vt, int64_t cap_vt, int32_t* faces,
+                                 int64_t cap_faces, int64_t counts[3])
+{
+  if (!path || !counts) {
+    dth::set_error("null argument");
+    return DT_E_INVALID;
+  }
+  ObjMesh m;
+  std::string err;
+  if (!load_obj(path, m, err)) {
+    dth::set_error(err);
+    return DT_E_IO;
+  }
+  const int64_t nv = (int64_t)m.v.size(), nt = (int64_t)m.vt.size() / 2, nf = (int64_t)m.vi.size() / 3;
+  counts[0] = nv;
+  counts[1] = nt;
+  counts[2] = nf;
+  if (v && cap_v >= nv)
+    for (int64_t i = 0; i < nv; ++i) {
+      v[3 * i] = (float)m.v[i].x;
+      v[3 * i + 1] = (float)m.v[i].y;
+      v[3 * i + 2] = (float)m.v[i].z;
+    }
+  if (vt && cap_vt >= nt)
+    for (int64_t i = 0; i < 2 * nt; ++i) vt[i] = (float)m.vt[i];
+  if (faces && cap_faces >= nf)
+    for (int64_t f = 0; f < nf; ++f)
+      for (int k = 0; k < 3; ++k) {
+        faces[6 * f + k] = m.vi[3 * f + k];
+        faces[6 * f + 3 + k] = m.ti[3 * f + k];
+      }
+  return DT_OK;
+}

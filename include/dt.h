@@ -351,6 +351,13 @@ void dt_scene_desc_free(dt_scene_desc* d);
 int dt_mocap_bone_table(const char* asf, const char* amc, const int32_t* frames, int32_t n_frames,
                         double* out, int32_t* n_bones, int32_t* n_postures);
 
+/* test hook: the OBJ ingest of finalBuildModels (loadObj, objHelper.h:6-85) on one file. counts =
+ * {vertices, texcoords, triangles}; with capacities >= those, v gets 3 floats per vertex, vt 2 per
+ * texcoord and faces 6 int32 per triangle (3 vertex + 3 texcoord indices, 0-based, -1: none).
+ * Null arrays only report the counts. */
+int dt_debug_load_obj(const char* path, float* v, int64_t cap_v, float* vt, int64_t cap_vt, int32_t* faces,
+                      int64_t cap_faces, int64_t counts[3]);
+
 /* writePPM (helpers.h:174-195): float -> unsigned char truncation */
 int dt_write_ppm(const char* filename, int32_t xRes, int32_t yRes, const float* values);
 /* the same pixels as an 8-bit RGB PNG (the output surface beside PPM) */
