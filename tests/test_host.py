@@ -125,7 +125,8 @@ def test_oracle_prismcyl_hole_and_face():
 
 @pytest.mark.parametrize("name,frame,models", [("final", 240, 0), ("spheres", 0, 0), ("dof", 0, 0), ("hw4", 0, 0),
                                                ("prismcyl", 3, 0), ("final", 0, 0), ("final", 480, 0), ("final", 2000, 0),
-                                               ("final", 480, 1), ("final", 1200, 0), ("final", 1680, 0)])
+                                               ("final", 480, 1), ("final", 240, 1), ("final", 1200, 0),
+                                               ("final", 1680, 0)])
 def test_bvh_topology_equals_oracle(name, frame, models):
     g = dt.globals_default()
     g.use_model = models
