@@ -533,6 +533,11 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   };
   auto test_rows = [&](size_t l, Band& band, int row_lo, int row_hi, long& dropped_n) {
     std::vector<std::pair<int32_t, int32_t>> pr;   // (cell, leaf), each cell's leaves in leaf order
+    // leaves listed so far per cell of the band: a cell past max_list walks the tree whatever else
+    // is listed (the packing below), so its remaining (leaf, cell) tests are skipped. Umbra cells
+    // are decided by umbra_rows alone. (Lists are not reordered then: order_lists needs them whole.)
+    const size_t band_lo = (size_t)row_lo * g.dim[0];
+    std::vector<int32_t> listed(order_lists ? 0 : (size_t)(row_hi - row_lo) * g.dim[0], 0);
     const dtd::DLight& L = lights[l];
     const LightSetup& S = ls[l];
     const double* llo = S.llo;
@@ -604,10 +609,13 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
               const int row = z * g.dim[1] + y;
               if (row < row_lo || row >= row_hi) continue;
               for (int x = xb; x <= xe; ++x) {
+                const size_t cell = (size_t)row * g.dim[0] + x;
+                if (!listed.empty() && listed[cell - band_lo] > max_list) continue;
                 cell_box(x, y, z, x, y, z, clo, chi);
                 if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
                 if (block_sep || separated(clo, chi, 2)) { ++dropped_n; continue; }
-                pr.push_back({(int32_t)((size_t)row * g.dim[0] + x), leaf});
+                pr.push_back({(int32_t)cell, leaf});
+                if (!listed.empty()) ++listed[cell - band_lo];
               }
             }
           }
