@@ -1,0 +1,95 @@
+"""GPU parity at the edges of the render loop's input space: image sizes that are
+not multiples of the tile (ragged right and top tiles), single-pixel and single-row images,
+antialias_samples that are not perfect squares (the reference takes int(sqrt(n))^2 samples,
+render_final_project.cpp:1040-1046), depth 1 and the configs' depths, and a tile split with more
+ranks than tiles (ranks whose slab holds no pixel). Every case is compared with the CPU oracle
+bit for bit on the same seeds (max|diff| = 0; north_star's 1e-4 tolerance is the bound written
+in the assertion), and the work counters must match the reference loop's.
+"""
+import numpy as np
+import pytest
+import torch
+
+import distraytracer_amd as dt
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def _render_both(built, g, frame, tile):
+    n = dt.slab_floats(g, tile) if tile.layout == dt.DT_OUT_SLAB else 3 * g.xRes * g.yRes
+    scene = dt.Scene(built, g)
+    out = torch.zeros(max(n, 1), dtype=torch.float32, device="cuda")
+    st = dt.render(scene, g, frame, out, tile)
+    scene.close()
+    gpu = out.cpu().numpy()[:n]
+    ref, rst = oracle.render(built, g, frame, tile, out=np.zeros(max(n, 1), dtype=np.float32))
+    return gpu, ref[:n], st, rst
+
+
+def _assert_same(label, gpu, ref, st, rst):
+    diff = np.abs(gpu.astype(np.float64) - ref.astype(np.float64)) if gpu.size else np.zeros(1)
+    print("%s: pixels=%d samples=%d rays=%d max|diff|=%.3g" % (label, st.pixels, st.samples, st.rays,
+                                                              float(diff.max())))
+    assert st.pixels == rst.pixels and st.samples == rst.samples
+    assert st.rays == rst.rays and st.shadow_rays == rst.shadow_rays
+    assert st.stack_overflows == 0 and st.nan_pixels == rst.nan_pixels
+    assert not np.isnan(gpu).any()
+    assert float(diff.max()) <= TOL, "%s: max|diff| %.3g > %g" % (label, float(diff.max()), TOL)
+
+
+# (W, H, antialias_samples, depth): spp = int(sqrt(aa))^2
+SIZES = [(1, 1, 4, 2), (7, 5, 10, 3), (33, 17, 2, 1), (97, 3, 16, 4), (2, 41, 9, 8)]
+
+
+@pytest.mark.parametrize("W,H,aa,depth", SIZES)
+def test_ragged_sizes_spheres(cuda, W, H, aa, depth):
+    """buildSceneSpheres(0) (C1's scene, motion-blurred spheres) at sizes that leave partial
+    tiles, in the image layout with 32x32 tiles."""
+    g = dt.globals_default()
+    built = dt.build_scene("spheres", 0, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = W, H, aa, depth
+    gpu, ref, st, rst = _render_both(built, g, 0, dt.tiles())
+    assert st.pixels == W * H
+    assert st.samples == W * H * int(int(aa ** 0.5) ** 2)
+    _assert_same("spheres %dx%d aa=%d depth=%d" % (W, H, aa, depth), gpu, ref, st, rst)
+
+
+@pytest.mark.parametrize("W,H,aa,depth", [(13, 9, 4, 8), (70, 1, 2, 4)])
+def test_ragged_sizes_final(cuda, W, H, aa, depth):
+    """buildFinal(240) (the C2/C3 scene: glossy cascades, area lights, textures) at ragged sizes."""
+    g = dt.globals_default()
+    g.use_model = 0
+    built = dt.build_scene("final", 240, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = W, H, aa, depth
+    gpu, ref, st, rst = _render_both(built, g, 240, dt.tiles(tile_w=8, tile_h=8))
+    _assert_same("final %dx%d aa=%d depth=%d" % (W, H, aa, depth), gpu, ref, st, rst)
+
+
+def test_more_ranks_than_tiles(cuda):
+    """20x12 in 8x8 tiles is 3x2 = 6 tiles (ragged on both axes); split over 8 ranks, two ranks own
+    no tile. Every rank's slab matches the oracle's, the empty ranks render nothing, and the
+    unpacked slabs give the single-GPU image."""
+    g = dt.globals_default()
+    g.use_model = 0
+    built = dt.build_scene("final", 240, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = 20, 12, 4, 4
+    world = 8
+    base = dt.tiles(tile_w=8, tile_h=8, rank=0, world=world, layout=dt.DT_OUT_SLAB)
+    slab_n = dt.slab_floats_max(g, base)
+    slabs = np.zeros(world * slab_n, dtype=np.float32)
+    empty = 0
+    for r in range(world):
+        tile = dt.tiles(tile_w=8, tile_h=8, rank=r, world=world, layout=dt.DT_OUT_SLAB)
+        gpu, ref, st, rst = _render_both(built, g, 240, tile)
+        _assert_same("rank %d of %d" % (r, world), gpu, ref, st, rst)
+        empty += st.pixels == 0
+        slabs[r * slab_n:r * slab_n + gpu.size] = gpu
+    assert empty == 2
+    image = torch.zeros(3 * 20 * 12, dtype=torch.float32, device="cuda")
+    dt.unpack_slabs(g, base, world, torch.from_numpy(slabs).cuda(), image)
+    torch.cuda.synchronize()
+    whole, ref, st, rst = _render_both(built, g, 240, dt.tiles())
+    assert np.array_equal(image.cpu().numpy(), whole)
