@@ -133,7 +133,7 @@ def valu_roofline(cfg, kernel_ms, samples, ref_work=None, ref_samples=0):
     r = {"bound": "valu", "achieved": round(achieved, 4), "peak": W.PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
          "frac": achieved / W.PEAK_FP64_TFLOPS,
          "ops_per_launch": ops, "ops_per_sample": round(ops / samples, 2),
-         "kernel": "dt_trace_kernel", "kernel_ms": round(kernel_ms, 3),
+         "kernel": None, "kernel_ms": round(kernel_ms, 3),   # named by the caller
          "counts_per_sample": W.breakdown(dev["counts"], dev["samples"]),
          "note": "FP64-equivalent VALU operations of the events the kernel executes (include/dt_work.h "
                  "weights x libdt_work.so counts). Every operation is unfused (no FMA contraction, for "
@@ -147,6 +147,13 @@ def valu_roofline(cfg, kernel_ms, samples, ref_work=None, ref_samples=0):
                                "note": "the reference's own loop (every leaf its boxes pass, the sky per "
                                        "missing sample), counted by the oracle on the cpu_baseline sample"}
     return r
+
+
+def trace_kernel_name(spp):
+    """the trace kernel dt_render launches for this spp (dt_api.cpp enqueue_render: the 5-wave build
+    at one pixel per wave, spp >= 64, unless DT_W5 says otherwise)"""
+    e = os.environ.get("DT_W5")
+    return "dt_trace_kernel_w5" if (e[:1] == "1" if e else spp >= 64) else "dt_trace_kernel"
 
 
 def load_pmc_traffic():
@@ -291,8 +298,10 @@ def main():
         roof = None
         if world == 1 and not args.no_roofline:
             roof = valu_roofline(args.config, kernel_ms, W * H * spp, ref_work, ref_samples)
+        if roof is not None:
+            roof["kernel"] = trace_kernel_name(spp)
         if roof is None:   # no diagnostic library (or N > 1): the HBM line alone
-            roof = dict(hbm, kernel="dt_trace_kernel", kernel_ms=round(kernel_ms, 3))
+            roof = dict(hbm, kernel=trace_kernel_name(spp), kernel_ms=round(kernel_ms, 3))
         else:
             roof["hbm"] = hbm
         if pmc.get("valu_active_per_wave_cycle"):

@@ -30,6 +30,8 @@ extern "C" const void* dt_trace_kernel_rpc_ptr(void);
 extern "C" hipError_t dt_launch_trace_dn(const void* dev_launch, float* out, int grid, hipStream_t stream);
 extern "C" hipError_t dt_launch_normalize(const double* in, double* out, int64_t n, hipStream_t stream);
 extern "C" const void* dt_trace_kernel_dn_ptr(void);
+extern "C" hipError_t dt_launch_trace_w5(const void* dev_launch, float* out, int grid, hipStream_t stream);
+extern "C" const void* dt_trace_kernel_w5_ptr(void);
 extern "C" hipError_t dt_launch_isect(const void* dev_launch, int64_t first, int64_t n, int32_t* hit_shape, float* hit_t,
                                       int grid, hipStream_t stream);
 extern "C" const void* dt_isect_kernel_ptr(void);
@@ -654,11 +656,17 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   // when DT_DONATE=1; its pre-order paths hold 10 levels of 3 bits (max_depth <= 11, brdf_samples <= 6)
   const char* dn_env = getenv("DT_DONATE");
   const bool donate = !sc->no_cull && dn_env && dn_env[0] == '1' && P.max_depth <= 11 && P.brdf_samples <= 6;
-  static int resident = 0, resident_rpc = 0, resident_dn = 0;
+  // one pixel per wave (spp >= 64) takes the 5-waves-per-SIMD build (dt_kernels.hip DT_W5): C3 +1.8%,
+  // C4 +4%; with several pixels per wave (C2, 16 spp) it loses 8% (profiles/r03ba_ab_w5.log).
+  // DT_W5=0 never, DT_W5=1 at any spp.
+  const char* w5_env = getenv("DT_W5");
+  const bool w5 = !sc->no_cull && !donate && (w5_env ? w5_env[0] == '1' : P.spp >= 64);
+  static int resident = 0, resident_rpc = 0, resident_dn = 0, resident_w5 = 0;
   if (!resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
   if (sc->no_cull && !resident_rpc) resident_rpc = max_resident_waves(dt_trace_kernel_rpc_ptr(), 64);
   if (donate && !resident_dn) resident_dn = max_resident_waves(dt_trace_kernel_dn_ptr(), 64);
-  const int64_t waves = sc->no_cull ? resident_rpc : donate ? resident_dn : resident;
+  if (w5 && !resident_w5) resident_w5 = max_resident_waves(dt_trace_kernel_w5_ptr(), 64);
+  const int64_t waves = sc->no_cull ? resident_rpc : donate ? resident_dn : w5 ? resident_w5 : resident;
   int64_t grid = P.n_items < waves ? P.n_items : waves;
   if (grid < 1) grid = 1;
   hs.dn_pool = nullptr;
@@ -720,6 +728,7 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   HIPCHK(hipEventRecord(sc->ev0, st));
   HIPCHK(sc->no_cull ? dt_launch_trace_rpc(sc->d_launch, out_dev, (int)grid, st)
          : donate   ? dt_launch_trace_dn(sc->d_launch, out_dev, (int)grid, st)
+         : w5       ? dt_launch_trace_w5(sc->d_launch, out_dev, (int)grid, st)
                     : dt_launch_trace(sc->d_launch, out_dev, (int)grid, st));
   if (PL.sky_defer) HIPCHK(dt_launch_sky_miss(sc->d_launch, out_dev, n_px, st));
   HIPCHK(hipEventRecord(sc->ev1, st));

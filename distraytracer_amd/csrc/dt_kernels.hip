@@ -79,8 +79,15 @@ using namespace dtd;
 #ifndef DT_ISECT
 #define DT_ISECT 0
 #endif
+// DT_W5=1 (build/dt_kernels_w5.o): the trace kernel at 5 waves per SIMD (96 VGPRs, under 8 KiB of
+// LDS per wave: DT_NREC_CCOL=1, DT_PSUM_LDS=0), launched for one-pixel-per-wave work (spp >= 64)
+#ifndef DT_W5
+#define DT_W5 0
+#endif
 #if DT_WITH_RPC
 #define DT_TRACE_KERNEL dt_trace_kernel_rpc
+#elif DT_W5
+#define DT_TRACE_KERNEL dt_trace_kernel_w5
 #elif DT_DONATE
 #define DT_TRACE_KERNEL dt_trace_kernel_dn
 #else
@@ -124,6 +131,12 @@ using namespace dtd;
 #define DT_SG_MIXED 0      // waves with lanes outside the lists: union for the others, then tree walk
                            // (C3 +0.9%, C4 -3.2%, profiles/r03t; split only when no cell walks the tree:
                            // C3 +-0.1%, profiles/r03v)
+#endif
+#ifndef DT_NREC_CCOL
+#define DT_NREC_CCOL 0  // the shading record keeps the hit's colour offset, not its colour (1024 B less LDS)
+#endif
+#ifndef DT_PSUM_LDS
+#define DT_PSUM_LDS 1   // per-pixel sums in LDS (0: a register triple, 1536 B less LDS per wave)
 #endif
 #ifndef DT_LS_CACHE
 #define DT_LS_CACHE 4   // lights whose area-sample pair is kept in LDS between the two light passes
@@ -2508,7 +2521,11 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
       if (walk) {
         nrec[0][ln_] = normal.x; nrec[1][ln_] = normal.y; nrec[2][ln_] = normal.z;
         nrec[3][ln_] = eye.x; nrec[4][ln_] = eye.y; nrec[5][ln_] = eye.z;
+#if DT_NREC_CCOL
+        ((int*)&nrec[6][0])[ln_] = h.ccol;   // the colour is re-read from its record in pass 2
+#else
         nrec[6][ln_] = shape_color.x; nrec[7][ln_] = shape_color.y; nrec[8][ln_] = shape_color.z;
+#endif
       }
       asm volatile("" ::: "memory");
       uint32_t vis = 0;
@@ -2558,7 +2575,12 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
         if (vis != 0) {
           nrm = v3(nrec[0][ln_], nrec[1][ln_], nrec[2][ln_]);
           eye2 = v3(nrec[3][ln_], nrec[4][ln_], nrec[5][ln_]);
+#if DT_NREC_CCOL
+          const int cc = ((const int*)&nrec[6][0])[ln_];
+          shape_color = cc >= 0 ? G3(cas(S.geom) + S.hdr[sid].off, cc) : v3a(S.mat[sid].color);
+#else
           shape_color = v3(nrec[6][ln_], nrec[7][ln_], nrec[8][ln_]);
+#endif
         }
         const DMat* Mp = S.mat + sid;
         const V3 e_dir = normalized(sub(eye2, isectP));
@@ -2830,11 +2852,13 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   // (inside run_pass only); red (per-chunk sample colours) and dens (cloud march chunk) are
   // used after the passes, so they share its space. ocol: the DFS colour accumulator,
   // psum: the per-pixel sums, parked here instead of in registers across the DFS.
-  __shared__ double nrec[9][DT_WAVE];
+  __shared__ double nrec[DT_NREC_CCOL ? 7 : 9][DT_WAVE];
   double* const red = &nrec[0][0];                        // DT_WAVE * 3 doubles
   float* const dens = (float*)(&nrec[0][0] + DT_WAVE * 3);  // DT_CLOUD_CHUNK floats
   __shared__ double ocol[3][DT_WAVE];
+#if DT_PSUM_LDS
   __shared__ double psum[3][DT_WAVE];
+#endif
   __shared__ double chan[4];
   __shared__ float lsxy[DT_LS_CACHE > 0 ? DT_LS_CACHE : 1][2][DT_WAVE];
   __shared__ unsigned long long item_s;
@@ -2895,7 +2919,11 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     // lanes: pixel slot j = lane / min(spp,64), sample = chunk*64 + lane % ...
     const int per = spp < DT_WAVE ? spp : DT_WAVE;
     const int j = lane / per;
+#if DT_PSUM_LDS
     psum[0][lane] = 0; psum[1][lane] = 0; psum[2][lane] = 0;   // lane j (< group): pixel j, sample order
+#else
+    V3 psr = v3(0, 0, 0);   // lane j (< group): pixel j's sum, in sample order
+#endif
     int px_x = 0, px_y = 0;
     int64_t px_off = 0;
     bool px_valid = false;
@@ -3002,9 +3030,17 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         int ns = spp - chunk * DT_WAVE;
         if (ns > per) ns = per;
         {
+#if DT_PSUM_LDS
           V3 ps = v3(psum[0][lane], psum[1][lane], psum[2][lane]);
+#else
+          V3 ps = psr;
+#endif
           for (int s = 0; s < ns; ++s) ps = add(ps, v3(red[(base + s) * 3], red[(base + s) * 3 + 1], red[(base + s) * 3 + 2]));
+#if DT_PSUM_LDS
           psum[0][lane] = ps.x; psum[1][lane] = ps.y; psum[2][lane] = ps.z;
+#else
+          psr = ps;
+#endif
         }
       }
       __syncthreads();
@@ -3016,7 +3052,11 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       bool qv;
       pixel_of(P, item * group + lane, qx, qy, qo, qv);
       if (qv && !(P.sky_defer && S.sky_miss[item * group + lane])) {
+#if DT_PSUM_LDS
         V3 color = divs(v3(psum[0][lane], psum[1][lane], psum[2][lane]), spp);
+#else
+        V3 color = divs(psr, spp);
+#endif
 #ifdef DT_ITEM_TIMES   // diagnostic builds (tools/item_times.py): the item's wave cycles / 1e4, raw
         {
           const float cyc = (float)(__builtin_amdgcn_s_memtime() - item_t0) * 1e-4f;
@@ -3062,7 +3102,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
 
 #endif   // !DT_ISECT
 
-#if !DT_WITH_RPC && !DT_DONATE && !DT_ISECT
+#if !DT_WITH_RPC && !DT_DONATE && !DT_ISECT && !DT_W5
 // The sky of the pixels a 1-spp trace launch flagged as missed (P.sky_defer): renderImage's miss
 // branch (cpp:1074-1092: cloudColor of mcam * focalPoint) one pixel per lane, at the occupancy of a
 // small kernel instead of inside the trace kernel's register budget. With one sample the pixel is
@@ -3205,6 +3245,14 @@ extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_
 }
 extern "C" const void* dt_trace_kernel_ptr(void) { return (const void*)dt_trace_kernel; }
 #elif DT_ISECT
+#elif DT_W5   // the trace kernel at 5 waves per SIMD
+static_assert(DT_TRACE_MIN_WAVES == 5 && DT_NREC_CCOL && !DT_PSUM_LDS, "dt_kernels_w5.o: Makefile flags");
+extern "C" hipError_t dt_launch_trace_w5(const void* dev_launch, float* out, int grid, hipStream_t stream)
+{
+  hipLaunchKernelGGL(dt_trace_kernel_w5, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
+  return hipGetLastError();
+}
+extern "C" const void* dt_trace_kernel_w5_ptr(void) { return (const void*)dt_trace_kernel_w5; }
 #elif DT_DONATE   // the trace kernel with DFS work sharing inside the wave
 extern "C" hipError_t dt_launch_trace_dn(const void* dev_launch, float* out, int grid, hipStream_t stream)
 {

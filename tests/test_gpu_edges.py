@@ -93,3 +93,22 @@ def test_more_ranks_than_tiles(cuda):
     torch.cuda.synchronize()
     whole, ref, st, rst = _render_both(built, g, 240, dt.tiles())
     assert np.array_equal(image.cpu().numpy(), whole)
+
+
+@pytest.mark.parametrize("aa,depth", [(64, 8), (16, 4)])
+def test_five_wave_kernel_matches(cuda, monkeypatch, aa, depth):
+    """dt_trace_kernel_w5 (5 waves per SIMD, DT_W5; the default at spp >= 64) and the 4-wave
+    dt_trace_kernel render the same bits, at one and at four pixels per wave; checked against the
+    oracle as well."""
+    g = dt.globals_default()
+    g.use_model = 0
+    built = dt.build_scene("final", 240, g)
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = 1920, 1080, aa, depth
+    tile = dt.tiles(tile_w=8, tile_h=8, rank=3, world=256, layout=dt.DT_OUT_SLAB)
+    imgs = []
+    for w5 in ("0", "1"):
+        monkeypatch.setenv("DT_W5", w5)
+        gpu, ref, st, rst = _render_both(built, g, 240, tile)
+        _assert_same("DT_W5=%s aa=%d" % (w5, aa), gpu, ref, st, rst)
+        imgs.append(gpu)
+    assert np.array_equal(imgs[0], imgs[1])

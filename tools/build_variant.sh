@@ -12,5 +12,5 @@ CG=${CODEGEN--mllvm -disable-machine-licm -mllvm -disable-machine-cse -mllvm -di
 /opt/rocm/bin/hipcc -I"$C" -DDT_TRACE_MIN_WAVES=${W:-4} $CG "$@" --offload-arch=gfx950 -O3 -std=c++17 -fPIC \
   -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -c "$src" -o "$C/build/var/k_$name.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/distraytracer_amd/variants/libdt_$name.so" \
-  "$C/build/var/k_$name.o" "$C"/build/dt_kernels_rpc.o "$C"/build/dt_kernels_dn.o "$C"/build/dt_kernels_isect.o "$C"/build/dt_api.o "$C"/build/host_*.o
+  "$C/build/var/k_$name.o" "$C"/build/dt_kernels_w5.o "$C"/build/dt_kernels_rpc.o "$C"/build/dt_kernels_dn.o "$C"/build/dt_kernels_isect.o "$C"/build/dt_api.o "$C"/build/host_*.o
 echo "built variants/libdt_$name.so"

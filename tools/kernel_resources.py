@@ -45,6 +45,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     build = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "distraytracer_amd", "csrc", "build")
     ap.add_argument("objects", nargs="*", default=[os.path.join(build, "dt_kernels.o"),
+                                                   os.path.join(build, "dt_kernels_w5.o"),
                                                    os.path.join(build, "dt_kernels_rpc.o"),
                                                    os.path.join(build, "dt_kernels_dn.o"),
                                                    os.path.join(build, "dt_kernels_isect.o")])
