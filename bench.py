@@ -313,7 +313,7 @@ def main():
         if pmc.get("valu_active_per_wave_cycle"):
             roof["pmc"] = {"profile": "profiles/%s_summary.json" % pmc.get("tag"),
                            "valu_active_per_wave_cycle": pmc.get("valu_active_per_wave_cycle"),
-                           "simd_busy": round(4 * pmc["valu_active_per_wave_cycle"], 3),
+                           "simd_busy": round(pmc.get("waves_per_simd", 4) * pmc["valu_active_per_wave_cycle"], 3),
                            "lane_utilisation": pmc.get("valu_lane_utilisation")}
         line = {
             "metric": "Mpixel-samples/s (W×H×spp/s) + wall-clock per frame, 1/2/4/8 GPU",

@@ -42,6 +42,8 @@ def main(tag, kernel="dt_trace_kernel"):
         out["write_kib"] = per["WRITE_SIZE"]
     if "SQ_ACTIVE_INST_VALU" in per and "SQ_WAVE_CYCLES" in per:
         out["valu_active_per_wave_cycle"] = per["SQ_ACTIVE_INST_VALU"] / per["SQ_WAVE_CYCLES"]
+    if "SQ_WAVES" in per:   # persistent grid: the resident waves per SIMD (256 CUs x 4 SIMDs)
+        out["waves_per_simd"] = per["SQ_WAVES"] / 1024
     if "SQ_THREAD_CYCLES_VALU" in per and "SQ_ACTIVE_INST_VALU" in per:
         out["valu_lane_utilisation"] = per["SQ_THREAD_CYCLES_VALU"] / (64 * per["SQ_ACTIVE_INST_VALU"])
     f64 = sum(per.get(k, 0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_TRANS_F64"))
@@ -57,7 +59,7 @@ def main(tag, kernel="dt_trace_kernel"):
     # the profile bench.py's roofline.traffic reads (the latest summarised tag)
     with open(os.path.join(ROOT, "profiles", "pmc_trace_summary.json"), "w") as fh:
         json.dump({k: out.get(k) for k in ("tag", "kernel", "avg_duration_ns", "hbm_bytes_per_launch",
-                                            "valu_active_per_wave_cycle", "valu_lane_utilisation",
+                                            "valu_active_per_wave_cycle", "valu_lane_utilisation", "waves_per_simd",
                                             "fp64_tflops_upper")},
                   fh, indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
