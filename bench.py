@@ -159,7 +159,8 @@ def trace_kernel_name(spp):
     """the trace kernel dt_render launches for this spp (dt_api.cpp enqueue_render: the 5-wave build
     at one pixel per wave, spp >= 64, unless DT_W5 says otherwise)"""
     e = os.environ.get("DT_W5")
-    return "dt_trace_kernel_w5" if (e[:1] == "1" if e else spp >= 64) else "dt_trace_kernel"
+    ppw = 64 // min(spp, 64)
+    return "dt_trace_kernel_w5" if ppw <= 8 and (e[:1] == "1" if e else spp >= 64) else "dt_trace_kernel"
 
 
 def load_pmc_traffic():

@@ -658,9 +658,9 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   const bool donate = !sc->no_cull && dn_env && dn_env[0] == '1' && P.max_depth <= 11 && P.brdf_samples <= 6;
   // one pixel per wave (spp >= 64) takes the 5-waves-per-SIMD build (dt_kernels.hip DT_W5): C3 +1.8%,
   // C4 +4%; with several pixels per wave (C2, 16 spp) it loses 8% (profiles/r03ba_ab_w5.log).
-  // DT_W5=0 never, DT_W5=1 at any spp.
+  // DT_W5=0 never, DT_W5=1 at any spp with at most 8 pixels per wave (its per-pixel sums have 8 slots).
   const char* w5_env = getenv("DT_W5");
-  const bool w5 = !sc->no_cull && !donate && (w5_env ? w5_env[0] == '1' : P.spp >= 64);
+  const bool w5 = !sc->no_cull && !donate && P.ppw <= 8 && (w5_env ? w5_env[0] == '1' : P.spp >= 64);
   static int resident = 0, resident_rpc = 0, resident_dn = 0, resident_w5 = 0;
   if (!resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
   if (sc->no_cull && !resident_rpc) resident_rpc = max_resident_waves(dt_trace_kernel_rpc_ptr(), 64);

@@ -80,7 +80,8 @@ using namespace dtd;
 #define DT_ISECT 0
 #endif
 // DT_W5=1 (build/dt_kernels_w5.o): the trace kernel at 5 waves per SIMD (96 VGPRs, under 8 KiB of
-// LDS per wave: DT_NREC_CCOL=1, DT_PSUM_LDS=0), launched for one-pixel-per-wave work (spp >= 64)
+// LDS per wave: DT_NREC_CCOL=1, DT_PSUM_LDS=2), launched for one-pixel-per-wave work (spp >= 64; never
+// with more than 8 pixels per wave, the slots DT_PSUM_LDS=2 keeps)
 #ifndef DT_W5
 #define DT_W5 0
 #endif
@@ -2857,7 +2858,8 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   float* const dens = (float*)(&nrec[0][0] + DT_WAVE * 3);  // DT_CLOUD_CHUNK floats
   __shared__ double ocol[3][DT_WAVE];
 #if DT_PSUM_LDS
-  __shared__ double psum[3][DT_WAVE];
+  // DT_PSUM_LDS=2: slots for up to 8 pixels per wave only (spp >= 8; 192 B instead of 1536 B)
+  __shared__ double psum[3][DT_PSUM_LDS == 2 ? 8 : DT_WAVE];
 #endif
   __shared__ double chan[4];
   __shared__ float lsxy[DT_LS_CACHE > 0 ? DT_LS_CACHE : 1][2][DT_WAVE];
@@ -2920,7 +2922,9 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     const int per = spp < DT_WAVE ? spp : DT_WAVE;
     const int j = lane / per;
 #if DT_PSUM_LDS
-    psum[0][lane] = 0; psum[1][lane] = 0; psum[2][lane] = 0;   // lane j (< group): pixel j, sample order
+    if (DT_PSUM_LDS == 1 || lane < 8) {   // lane j (< group): pixel j, sample order
+      psum[0][lane] = 0; psum[1][lane] = 0; psum[2][lane] = 0;
+    }
 #else
     V3 psr = v3(0, 0, 0);   // lane j (< group): pixel j's sum, in sample order
 #endif
@@ -3246,7 +3250,7 @@ extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_
 extern "C" const void* dt_trace_kernel_ptr(void) { return (const void*)dt_trace_kernel; }
 #elif DT_ISECT
 #elif DT_W5   // the trace kernel at 5 waves per SIMD
-static_assert(DT_TRACE_MIN_WAVES == 5 && DT_NREC_CCOL && !DT_PSUM_LDS, "dt_kernels_w5.o: Makefile flags");
+static_assert(DT_TRACE_MIN_WAVES == 5 && DT_NREC_CCOL && DT_PSUM_LDS == 2, "dt_kernels_w5.o: Makefile flags");
 extern "C" hipError_t dt_launch_trace_w5(const void* dev_launch, float* out, int grid, hipStream_t stream)
 {
   hipLaunchKernelGGL(dt_trace_kernel_w5, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
