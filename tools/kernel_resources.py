@@ -8,6 +8,7 @@ read with llvm-readelf; no GPU needed."""
 import json
 import os
 import re
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -20,7 +21,11 @@ KEYS = (".vgpr_count", ".agpr_count", ".sgpr_count", ".vgpr_spill_count", ".sgpr
 def resources(obj):
     with tempfile.TemporaryDirectory() as d:
         fat, hsaco = os.path.join(d, "fat.bin"), os.path.join(d, "k.hsaco")
-        subprocess.check_call(["objcopy", "--dump-section", ".hip_fatbin=" + fat, obj])
+        # objcopy rewrites its input when given no output file: dump from a scratch copy instead
+        # (leaves the build's objects, and make's view of them, untouched)
+        tmp_obj = os.path.join(d, "k.o")
+        shutil.copyfile(obj, tmp_obj)
+        subprocess.check_call(["objcopy", "--dump-section", ".hip_fatbin=" + fat, tmp_obj])
         subprocess.check_call([LLVM + "/clang-offload-bundler", "--type=o",
                                "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--input=" + fat,
                                "--output=" + hsaco, "--unbundle"])
