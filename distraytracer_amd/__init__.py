@@ -14,13 +14,13 @@ an error (there is no CPU path in this package).
 """
 import ctypes
 
-from ._lib import (DATA_DIR, DT_OUT_IMAGE, DT_OUT_SLAB, AccelInfo, BVHNode, DTError, Globals, SceneDesc,
+from ._lib import (DATA_DIR, DT_KERNEL_AUTO, DT_KERNEL_DONATE, DT_KERNEL_PRODUCT, DT_OUT_IMAGE, DT_OUT_SLAB, AccelInfo, BVHNode, DTError, Globals, SceneDesc,
                    Stats, Tiles, check, lib)
 
 __all__ = ["Globals", "Tiles", "Stats", "DTError", "globals_default", "build_scene", "Scene",
            "render", "render_sky", "renderImage", "renderImageCloud", "write_ppm", "DATA_DIR",
            "DT_OUT_IMAGE", "DT_OUT_SLAB", "slab_floats", "slab_floats_max", "unpack_slabs", "tiles", "check", "lib",
-           "accel_info"]
+           "accel_info", "DT_KERNEL_AUTO", "DT_KERNEL_PRODUCT", "DT_KERNEL_DONATE"]
 
 
 def globals_default():
@@ -84,6 +84,11 @@ class Scene:
 
     def upload(self):
         check(lib.dt_scene_upload(self._h), "dt_scene_upload")
+
+    def set_kernel(self, kernel):
+        """dt_scene_set_kernel: DT_KERNEL_AUTO (the DT_DONATE environment), DT_KERNEL_PRODUCT or
+        DT_KERNEL_DONATE for this scene's renders"""
+        check(lib.dt_scene_set_kernel(self._h, kernel), "dt_scene_set_kernel")
 
     @property
     def handle(self):

@@ -144,6 +144,7 @@ struct dt_scene {
   float bump_pad = 0;          // y padding of its leaves: the largest |shift| a blur pass can draw
   bool bump_up_only = false;   // bump tree / blur-padded lists built for shifts >= 0 only
   bool no_cull = false;        // a RectPrismWithCylinder: no t-culling, no grid, no primary lists
+  int kernel = DT_KERNEL_AUTO; // dt_scene_set_kernel
   ShadowGrid sg;
   void* d_sg_cells = nullptr;
   void* d_sg_list = nullptr;
@@ -188,6 +189,15 @@ struct dt_scene {
 extern "C" {
 
 int dt_abi_version(void) { return DT_ABI_VERSION; }
+
+int dt_scene_set_kernel(dt_scene* s, int32_t kernel)
+{
+  if (!s) return fail(DT_E_INVALID, "null scene");
+  if (kernel != DT_KERNEL_AUTO && kernel != DT_KERNEL_PRODUCT && kernel != DT_KERNEL_DONATE)
+    return fail(DT_E_INVALID, "dt_scene_set_kernel: unknown kernel choice");
+  s->kernel = kernel;
+  return DT_OK;
+}
 const char* dt_last_error(void) { return g_err.c_str(); }
 
 void dt_globals_default(dt_globals* g)
@@ -654,8 +664,10 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   // scenes with a RectPrismWithCylinder take the trace kernel compiled with its tests (dt_kernels.hip
   // DT_WITH_RPC), whose occupancy may differ. DFS work sharing inside the wave (dt_trace_kernel_dn)
   // when DT_DONATE=1; its pre-order paths hold 10 levels of 3 bits (max_depth <= 11, brdf_samples <= 6)
-  const char* dn_env = getenv("DT_DONATE");
-  const bool donate = !sc->no_cull && dn_env && dn_env[0] == '1' && P.max_depth <= 11 && P.brdf_samples <= 6;
+  // (dt_scene_set_kernel; DT_KERNEL_AUTO: the DT_DONATE environment variable)
+  const char* dn_env = sc->kernel == DT_KERNEL_AUTO ? getenv("DT_DONATE") : nullptr;
+  const bool want_dn = sc->kernel == DT_KERNEL_DONATE || (dn_env && dn_env[0] == '1');
+  const bool donate = !sc->no_cull && want_dn && P.max_depth <= 11 && P.brdf_samples <= 6;
   // one pixel per wave (spp >= 64) takes the 5-waves-per-SIMD build (dt_kernels.hip DT_W5): C3 +1.8%,
   // C4 +4%; with several pixels per wave (C2, 16 spp) it loses 8% (profiles/r03ba_ab_w5.log).
   // DT_W5=0 never, DT_W5=1 at any spp with at most 8 pixels per wave (its per-pixel sums have 8 slots).

@@ -99,58 +99,16 @@ using namespace dtd;
 #define DT_MAX_CLOUD_STEPS 2048
 #define DT_CLOUD_CHUNK 256
 #define DT_WAVE 64
-#ifndef DT_SLAB_MINMAX
-#define DT_SLAB_MINMAX 1   // min/max slab ends (exact with lb <= ub, P.boxes_ordered): +1% since the codegen flags
-#endif
-#ifndef DT_TCULL_HOIST
-#define DT_TCULL_HOIST 0   // 0: cull bound recomputed per node from the best t (+1.4% under the codegen flags)
-#endif
-#ifndef DT_FIN_PARTIAL
-#define DT_FIN_PARTIAL 1   // FINISH entries write/read only their colour and depth
-#endif
-#ifndef DT_ITEM_BATCH
-#define DT_ITEM_BATCH 0   // wave items per queue atomic; 0: P.item_batch (host: 2 for long runs, else 1)
-#endif
-#ifndef DT_SG_COHERENT
-#define DT_SG_COHERENT 1   // waves within reach of one cell test that cell's list (else: union path)
-#endif
-#ifndef DT_PRIO_STEPS
-#define DT_PRIO_STEPS 1    // 1: waves raise their issue priority after P.prio_steps DFS steps (dt_api.cpp)
-#endif
-#ifndef DT_PRIO_LEVEL
-#define DT_PRIO_LEVEL 3
-#endif
-#ifndef DT_LS_ORDINAL
-#define DT_LS_ORDINAL 1    // the sample-pair cache starts at the first area light (P.ls_first): C3 +0.6%
-#endif
-#if DT_LS_ORDINAL
-#define DT_LS_FIRST P.ls_first
-#else
-#define DT_LS_FIRST 0
-#endif
-#ifndef DT_SG_MIXED
-#define DT_SG_MIXED 0      // waves with lanes outside the lists: union for the others, then tree walk
-                           // (C3 +0.9%, C4 -3.2%, profiles/r03t; split only when no cell walks the tree:
-                           // C3 +-0.1%, profiles/r03v)
-#endif
+// Measured-and-dropped variants are not kept here (DESIGN.md §8 lists them with their A/B logs;
+// git history holds their code). The switches left select the four instantiations (Makefile).
+#define DT_PRIO_LEVEL 3    // issue priority of long DFS items (P.prio_steps, dt_api.cpp)
 #ifndef DT_NREC_CCOL
 #define DT_NREC_CCOL 0  // the shading record keeps the hit's colour offset, not its colour (1024 B less LDS)
 #endif
 #ifndef DT_PSUM_LDS
-#define DT_PSUM_LDS 1   // per-pixel sums in LDS (0: a register triple, 1536 B less LDS per wave)
+#define DT_PSUM_LDS 1   // per-pixel sums in LDS: 1 for up to 64 pixels per wave, 2 for up to 8 (DT_W5)
 #endif
-#ifndef DT_LS_CACHE
-#define DT_LS_CACHE 4   // lights whose area-sample pair is kept in LDS between the two light passes
-#endif
-#ifndef DT_FIN_LEAF
-#define DT_FIN_LEAF 1     // a node without children adds its own light at once instead of through a FINISH entry
-#endif
-#ifndef DT_LAZY_LIGHT
-#define DT_LAZY_LIGHT 0   // 1: its node key / k re-read inside the light loops (volatile loads): C3 -2.7% (r03f)
-#endif
-#ifndef DT_LAZY_ENTRY
-#define DT_LAZY_ENTRY 1   // the popped DFS entry's fields re-read from its stack slot where used (run_pass)
-#endif
+#define DT_LS_CACHE 4   // area lights whose sample pair is kept in LDS between the two light passes
 
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
        ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15,
@@ -223,31 +181,6 @@ __device__ __forceinline__ double pw_rt(double x, double y)
 {
   if (y >= 0 && y <= 64 && y == (double)(int)y) {
     int n = (int)y;
-#if DT_PHONG_DD
-    // double-double binary powering (exact products by fma): the rounded result matches glibc's
-    // pow for 99.9% of x instead of 21%
-    double rh = 1.0, rl = 0.0, bh = x, bl = 0.0;
-    while (n) {
-      if (n & 1) {
-        const double p = rh * bh;
-        double e = __builtin_fma(rh, bh, -p);
-        e = e + (rh * bl + rl * bh);
-        const double s = p + e;
-        rl = e - (s - p);
-        rh = s;
-      }
-      n >>= 1;
-      if (n) {
-        const double p = bh * bh;
-        double e = __builtin_fma(bh, bh, -p);
-        e = e + 2.0 * (bh * bl);
-        const double s = p + e;
-        bl = e - (s - p);
-        bh = s;
-      }
-    }
-    return rh + rl;
-#else
     double r = 1.0, b = x;
     while (n) {
       if (n & 1) r = r * b;
@@ -255,7 +188,6 @@ __device__ __forceinline__ double pw_rt(double x, double y)
       if (n) b = b * b;
     }
     return r;
-#endif
   }
   return pow(x, y);
 }
@@ -1222,13 +1154,8 @@ __device__ __forceinline__ bool box_hit_exact_finite(const DNodeDev& b, const Ra
   // host for every node, P.boxes_ordered, else every wave takes the general test) rounding is
   // monotone, so a <= c for inv > 0 and c <= a for inv < 0 -- the sign select of the
   // reference, without per-ray sign masks held in SGPRs across the walk.
-#if DT_SLAB_MINMAX
   const float tmin = fmaxf(fmaxf(fminf(ax, cx), fminf(ay, cy)), fminf(az, cz));
   const float tmax = fminf(fminf(fmaxf(ax, cx), fmaxf(ay, cy)), fmaxf(az, cz));
-#else
-  const float tmin = fmaxf(fmaxf(r.nx ? cx : ax, r.ny ? cy : ay), r.nz ? cz : az);
-  const float tmax = fminf(fminf(r.nx ? ax : cx, r.ny ? ay : cy), r.nz ? az : cz);
-#endif
   return (tmin <= tmax) & (tmax > 0) & (tmin <= tcull);
 }
 
@@ -1271,7 +1198,7 @@ __device__ __forceinline__ Walk make_walk(const DParams& P, bool active, V3 ray,
   w.rb = make_raybox(ray);
   const bool odd = w.rb.ix | w.rb.iy | w.rb.iz | isnan(ray.x) | isnan(ray.y) | isnan(ray.z) | isnan(st.x) |
                    isnan(st.y) | isnan(st.z);
-  w.inf_wave = __ballot(active && odd) != 0 || (DT_SLAB_MINMAX && !P.boxes_ordered);
+  w.inf_wave = __ballot(active && odd) != 0 || !P.boxes_ordered;
   w.bump_wave = __ballot(active && shift != 0.0f) != 0;
   return w;
 }
@@ -1377,9 +1304,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
     // finite-ray slab test (with the shrinking tcull) is monotone in the box, so a lane that
     // failed an ancestor fails here too (host_fasttree.cpp)
     const bool act = GENERAL ? resume <= i : active;
-#if !DT_TCULL_HOIST
     tcull = (h.t_min == FLT_MAX || (DT_WITH_RPC && P.no_cull)) ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
-#endif
     bool hb = act & node_hit<GENERAL>(w, nd, shift, org, tcull);
     DT_WORK(cnt.wnodes++);
     DT_WK(DT_WK_BOX, act);
@@ -1409,9 +1334,6 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
                 h.shape = sid;
                 h.inside = ins;
                 h.t_min = t_dist;
-#if DT_TCULL_HOIST
-                tcull = t_dist == FLT_MAX ? FLT_MAX : t_dist * 1.0001f + 1e-4f;
-#endif
                 h.ccol = cc;
               }
             }
@@ -1537,9 +1459,7 @@ __device__ __forceinline__ void shadow_leaf(const DScene& S, const DNodeDev& nd,
 #endif
     if (test) {
       DT_WK(DT_WK_SHADOW_SHAPE + type, true);
-#ifndef DT_ABL_NOPRIM_SHADOW
       if (shape_shadow(type, flags, cas(S.geom) + off, sn, sstart, t_max, shift)) occl = true;
-#endif
     }
 #ifdef DT_STAMPS
     cnt.ph[47 + (type & 7)] += __popcll(__ballot(test));
@@ -1579,9 +1499,6 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
   int resume = active ? 0 : 0x7fffffff;
   bool occl = false;
   const float tcull = (DT_WITH_RPC && P.no_cull) ? FLT_MAX : shadow_tcull(t_max);
-#ifdef DT_ABL_NOSHADOW
-  return false;
-#endif
   int i = 0;
 #ifdef DT_STAMPS
   unsigned long long nv = 0;
@@ -1716,9 +1633,6 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   // (umbra cells are only proven for shifts >= 0: with symmetric padding blur waves walk the tree)
   const bool bump_list = w.bump_wave && P.sg_ypad >= P.bump_pad && P.bump_up_only;
   if (w.bump_wave && !bump_list) return occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
-#ifdef DT_ABL_NOSHADOW
-  return false;
-#endif
   // Shadow grid: the first active lane's cell serves every lane within sg_reach cells of it.
   // Waves whose lanes all lie within that reach (coherent primary bounces) test the cell's
   // candidate list. Scattered waves (mostly glossy bounces) test the union of their lanes' own
@@ -1726,7 +1640,6 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   // walk); a wave with a lane outside the grid or in a cell whose list is too long walks the tree.
   // Measured slower for scattered waves: per-lane list walks with a per-lane shape switch (C3 1725
   // vs 1932, C4 843 vs 936 Mpixel-samples/s), the lists of two cells in turn.
-  bool occ_union = false;   // DT_SG_MIXED: lanes answered by the union walk
   // blur passes use the padded lists, pass-0 rays the unpadded ones when a second grid was built
   const int sg_b = w.bump_wave ? P.sg_base[li] : P.sg_base0[li];
   if (li < P.sg_n && sg_b >= 0) {
@@ -1744,7 +1657,7 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
     const bool near = (x >= x0 - r) & (x <= x0 + 1.0f + r) & (y >= y0 - r) & (y <= y0 + 1.0f + r) &
                       (z >= z0 - r) & (z <= z0 + 1.0f + r);
     DT_CNT(inside ? 36 : 38);
-    if (DT_SG_COHERENT && inside && !__ballot(active & !near)) {
+    if (inside && !__ballot(active & !near)) {
       const int c0 = ((int)z0 * P.sg_dim[1] + (int)y0) * P.sg_dim[0] + (int)x0;
       const DT_CAS uint32_t* e = cas(S.sg_cells) + 2 * (size_t)(sg_b + c0);
       const uint32_t off = e[0], n = e[1];
@@ -1759,7 +1672,6 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       }
       DT_CNT(37);
     }
-#ifndef DT_NO_SG_UNION
     {   // scattered waves: the union of the lanes' own cell lists, when every lane has one
       const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
       bool lin = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.sg_dim[0] && fy < (float)P.sg_dim[1] &&
@@ -1775,22 +1687,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       DT_CNT(40);
       if (!lin) ln = 0;
       loff &= ~DT_SG_UMBRA;   // an umbra cell's list holds its occluding face's leaf
+      // (a wave with some lanes outside the lists walks the tree for all of them: splitting it,
+      // the union for the others, measured C3 +0.9% and C4 -3.2%, profiles/r03t)
       const unsigned long long out_lanes = __ballot(active && !lin);
-#if DT_SG_MIXED
-      // lanes with a list take the union; the rest (outside the grid, or in a cell whose list is
-      // too long) walk the tree afterwards, unless the union already occluded them all
-      if (__ballot(active && lin)) {
-        DT_CNT(41);
-#ifdef DT_STAMPS
-        cnt.cur_path = 1;
-#endif
-        const bool o = bump_list ? occluded_union<true>(S, w, active && lin, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt)
-                                 : occluded_union<false>(S, w, active && lin, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
-        if (!out_lanes) return o;
-        active = active && !lin;
-        occ_union = o;
-      }
-#else
       if (!out_lanes) {
         DT_CNT(41);
 #ifdef DT_STAMPS
@@ -1799,15 +1698,13 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
         return bump_list ? occluded_union<true>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt)
                          : occluded_union<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
       }
-#endif
     }
-#endif
   }
 #ifdef DT_STAMPS
   cnt.cur_path = 2;
 #endif
-  if (w.bump_wave) return occ_union | occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
-  return occ_union | occluded_walk<0>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+  if (w.bump_wave) return occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+  return occluded_walk<0>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
 }
 
 // =====================================================================================
@@ -2069,9 +1966,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
   const DScene& S = *c.S;
   const DParams& P = *c.P;
   int sp = 0;
-#if DT_PRIO_STEPS > 0
   int prio_steps = 0;
-#endif
   if (active && P.max_depth > 0) {
     Entry e;
     e.a = ray0; e.b = org0; e.k = 1.0f; e.depth = P.max_depth; e.key = rootkey; e._pad = DT_ROOT_PAD;  // root
@@ -2144,8 +2039,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
 #if DT_DONATE
     bool waiting = false;   // a donated subtree's list is not complete yet
 #endif
-    Entry e;
-    int pidx = 0;   // DT_LAZY_ENTRY: the popped NODE entry's slot
+    int pidx = 0;   // the popped NODE entry's slot
 #if DT_DONATE
     while (sp > 0) {
       const int d = stack[--sp].depth;
@@ -2211,7 +2105,6 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
     if (!__ballot(have || waiting)) break;
 #else
     while (sp > 0) {
-#if DT_FIN_PARTIAL
       // read the depth word first: a FINISH entry only carries its colour
       const int d = stack[--sp].depth;
       if (d < 0) {
@@ -2221,34 +2114,14 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
         ocol[1][l] = ocol[1][l] + a.y;
         ocol[2][l] = ocol[2][l] + a.z;
       } else if (d > 0) {
-#if DT_LAZY_ENTRY
         pidx = sp;
-#else
-        e = stack[sp];
-#endif
         have = true;
         break;
       }
-#else
-      e = stack[--sp];
-      if (e.depth < 0) {
-        const int l = threadIdx.x & (DT_WAVE - 1);   // out.color += own light (in LDS)
-        ocol[0][l] = ocol[0][l] + e.a.x;
-        ocol[1][l] = ocol[1][l] + e.a.y;
-        ocol[2][l] = ocol[2][l] + e.a.z;
-      } else if (e.depth > 0) {
-#if DT_LAZY_ENTRY
-        pidx = sp;
-#endif
-        have = true;
-        break;
-      }
-#endif
     }
     if (!__ballot(have)) break;
 #endif
     DT_CNT(7);
-#if DT_PRIO_STEPS > 0
     // A deep glossy cascade (fan-out 2 per bounce, ~100 DFS steps for one lane against ~1.5 on
     // average; C3 has a column of such pixels) keeps its wave busy up to ~80x the mean item (7.6 ms
     // of wave time, tools/item_times.py): with the frame split over ranks that one wave bounds a
@@ -2256,31 +2129,14 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
     // end of the item). C3 at 8 ranks: slowest rank 7.45 -> 6.95 ms; at 1 rank it costs 0.5%, so
     // the host enables it for tile splits only (P.prio_steps).
     if (++prio_steps == P.prio_steps) __builtin_amdgcn_s_setprio(DT_PRIO_LEVEL);
-#endif
-#if DT_LAZY_ENTRY
     // The popped NODE entry stays in its stack slot until this step's FINISH record overwrites it
     // at the very end (the FINISH slot is that same slot), so its fields are read from there where
     // they are used, behind compiler barriers, instead of being held in registers across the walks:
     // the allocator spilled them to scratch right after the pop, a store of data already there.
+    // (re-reading node key and k inside the light loops as well measured C3 -2.7%, profiles/r03f)
 #define DT_EF(f) (stack[pidx].f)
-#if DT_LAZY_LIGHT
-    // node key and k of the entry, re-read (volatile: never replaced by a value held in a register)
-    // inside the light loops, whose every iteration holds a shadow walk
-#define DT_EF_NODE (*(volatile const uint32_t*)&stack[pidx].key)
-#define DT_EF_K (*(volatile const float*)&stack[pidx].k)
-#else
-#define DT_EF_NODE node
-#define DT_EF_K k
-#endif
     V3 ray = DT_EF(a), eye = DT_EF(b);
     const bool is_root = have && DT_EF(_pad) == DT_ROOT_PAD;
-#else
-    V3 ray = e.a, eye = e.b;
-    const int depth = e.depth;
-    const float k = e.k;
-    const uint32_t node = e.key;
-    const bool is_root = have && e._pad == DT_ROOT_PAD;
-#endif
 #if DT_DONATE
     // in_motion of the node with the largest pre-order path so far (own sample / current list)
     if (have) {
@@ -2310,14 +2166,12 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
       if (!__ballot(have && blk != b0)) pblock = b0;
     }
     bool any = closest_hit(S, P, have, ray, eye, shift, h, cnt, pblock);
-#if DT_LAZY_ENTRY
     asm volatile("" ::: "memory");   // the entry's fields: fresh loads, not values kept across the walk
     ray = DT_EF(a);
     eye = DT_EF(b);
     const int depth = DT_EF(depth);
     const float k = DT_EF(k);
     const uint32_t node = DT_EF(key);
-#endif
 #ifdef DT_STAMPS
     if (__ballot(is_root)) { cnt.ph[46] += cnt.ph[26] - v_before; cnt.ph[39] += 1; }
 #endif
@@ -2540,9 +2394,9 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
         if (walk) {
           DT_WK(DT_WK_LIGHT, true);
           // the first DT_LS_CACHE area lights park their sample pair in LDS for pass 2
-          const int slot = li - DT_LS_FIRST;
+          const int slot = li - P.ls_first;
           const bool cache = slot >= 0 && slot < DT_LS_CACHE;
-          sray = light_sample(c, L, li, isectP, DT_EF_NODE, S.stats + ST_SPHL, cache ? &lsxy[cache ? slot : 0][0][ln_] : nullptr,
+          sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL, cache ? &lsxy[cache ? slot : 0][0][ln_] : nullptr,
                               cache ? 1 : 0, pair);
           t_max = (float)norm(sray);
           sn = normalized(sray);
@@ -2611,9 +2465,9 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
 #ifdef DT_WORK_COUNTERS
           for (int m = 0; m < 4; ++m) DT_WK(DT_WK_BRDF + m, M.model == m);
 #endif
-          const int slot = li - DT_LS_FIRST;
+          const int slot = li - P.ls_first;
           const bool cache = slot >= 0 && slot < DT_LS_CACHE;
-          const V3 sray = light_sample(c, L, li, isectP, DT_EF_NODE, nullptr, cache ? &lsxy[cache ? slot : 0][0][ln_] : nullptr,
+          const V3 sray = light_sample(c, L, li, isectP, node, nullptr, cache ? &lsxy[cache ? slot : 0][0][ln_] : nullptr,
                                        cache ? 2 : 0);
           const V3 sn = normalized(sray);
           const V3 normal = nrm;
@@ -2624,11 +2478,6 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
           }
           V3 ray_col;
           const float roughness = M.roughness;
-#ifdef DT_ABL_NOBRDF
-          if (true) {
-            ray_col = cwise(shape_color, lc);
-          } else
-#endif
           if (M.model == DT_MODEL_OREN_NAYAR) {
             const float A = M.on_a, B = M.on_b;   // per material (host, cpp:896-897)
             float vn = (float)dot(e_dir, normal);
@@ -2641,12 +2490,6 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
             float f = A + B * angleDiff * cr_sinf(alpha) * cr_tanf(beta);
             ray_col = mul(f, mul(irradiance, cwise(shape_color, lc)));
           }
-#ifdef DT_ABL_NOCT
-          else if (M.model == DT_MODEL_COOK_TORRANCE) { ray_col = cwise(shape_color, lc); }
-#endif
-#ifdef DT_ABL_NOPHONG
-          else if (M.model == DT_MODEL_PHONG) { ray_col = cwise(shape_color, lc); }
-#endif
           else if (M.model == DT_MODEL_COOK_TORRANCE) {
             V3 H = normalized(add(e_dir, sray));
             float hn = (float)dmax(0.0, dot(normal, H));
@@ -2680,7 +2523,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
           }
           if (!is_approx_zero(ray_col)) {
             hits++;
-            tmp_color = add(tmp_color, mul(DT_EF_K, ray_col));
+            tmp_color = add(tmp_color, mul(k, ray_col));
           }
         }
         if (hits > 0) own = divs(tmp_color, hits);
@@ -2689,7 +2532,6 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
     DT_T(t6);
     DT_ACC(4, t3, t6);
     if (fin_slot >= 0) {
-#if DT_FIN_LEAF
       if (sp == fin_slot + 1) {
         // no children were pushed: the FINISH entry would be the very next pop, so the own light
         // goes into the accumulator now, in the same order, without a stack round trip
@@ -2702,17 +2544,9 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
         ocol[1][l] = ocol[1][l] + own.y;
         ocol[2][l] = ocol[2][l] + own.z;
 #endif
-      } else
-#endif
-      {
-#if DT_FIN_PARTIAL
-      stack[fin_slot].a = own;
-      stack[fin_slot].depth = -1;
-#else
-      Entry f;
-      f.a = own; f.b = v3(0, 0, 0); f.k = 0; f.depth = -1; f.key = 0; f._pad = 0;
-      stack[fin_slot] = f;
-#endif
+      } else {   // a FINISH entry: colour and depth only
+        stack[fin_slot].a = own;
+        stack[fin_slot].depth = -1;
       }
     }
   }
@@ -2905,9 +2739,9 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
 
   int64_t item = 0, batch_end = 0;
   while (true) {
-    // items are dequeued DT_ITEM_BATCH at a time (one same-address atomic per batch)
+    // items are dequeued P.item_batch at a time (one same-address atomic per batch)
     if (item >= batch_end) {
-      const int batch = DT_ITEM_BATCH > 0 ? DT_ITEM_BATCH : (P.item_batch > 1 ? P.item_batch : 1);
+      const int batch = P.item_batch > 1 ? P.item_batch : 1;
       if (lane == 0) item_s = atomicAdd(S.queue, (unsigned long long)batch);
       __syncthreads();
       item = (int64_t)item_s;
@@ -3073,9 +2907,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
       }
     }
-#if DT_PRIO_STEPS > 0
     if (P.prio_steps > 0) __builtin_amdgcn_s_setprio(0);
-#endif
     ++item;
   }
   {

@@ -30,43 +30,17 @@ DT_HD V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 DT_HD V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 DT_HD V3 mul(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
 DT_HD V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
-#if defined(DT_ABL_FASTDIV) && defined(__HIP_DEVICE_COMPILE__)
-// diagnostic builds only (inexact): the cost bound of the three IEEE divisions of a V3 by a scalar
-DT_HD V3 divs(V3 a, double s) { const double r = __builtin_amdgcn_rcp(s); return v3(a.x * r, a.y * r, a.z * r); }
-#else
 DT_HD V3 divs(V3 a, double s) { return v3(a.x / s, a.y / s, a.z / s); }
-#endif
 DT_HD double dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 DT_HD V3 cross(V3 a, V3 b)
 {
   return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 DT_HD double norm(V3 a) { return sqrt(dot(a, a)); }
-#if defined(DT_SHARED_RCP) && defined(__HIP_DEVICE_COMPILE__)
-// opt-in (measured slower): the three divisions of a normalisation with the divisor's
-// half of LLVM's f64 division sequence computed once (rcp + two Newton steps), exact when s lies in
-// [2^-400, 2^400] and each component is 0 or at least 2^-500 in magnitude (div_scale then scales
-// nothing and div_fmas is a plain fma); plain divisions otherwise. div_fixup keeps the specials.
-DT_HD V3 div_by_norm(V3 a, double s)
-{
-  const bool safe = (s >= 0x1p-400) & (s <= 0x1p400) & ((a.x == 0.0) | (fabs(a.x) >= 0x1p-500)) &
-                    ((a.y == 0.0) | (fabs(a.y) >= 0x1p-500)) & ((a.z == 0.0) | (fabs(a.z) >= 0x1p-500));
-  if (!safe) return v3(a.x / s, a.y / s, a.z / s);
-  double r = __builtin_amdgcn_rcp(s);
-  r = __builtin_fma(r, __builtin_fma(-s, r, 1.0), r);
-  r = __builtin_fma(r, __builtin_fma(-s, r, 1.0), r);
-  const double mx = a.x * r, my = a.y * r, mz = a.z * r;
-  return v3(__builtin_amdgcn_div_fixup(__builtin_fma(__builtin_fma(-s, mx, a.x), r, mx), s, a.x),
-            __builtin_amdgcn_div_fixup(__builtin_fma(__builtin_fma(-s, my, a.y), r, my), s, a.y),
-            __builtin_amdgcn_div_fixup(__builtin_fma(__builtin_fma(-s, mz, a.z), r, mz), s, a.z));
-}
-#else
-DT_HD V3 div_by_norm(V3 a, double s) { return divs(a, s); }
-#endif
 DT_HD V3 normalized(V3 a)
 {
   double n = dot(a, a);
-  if (n > 0) return div_by_norm(a, sqrt(n));
+  if (n > 0) return divs(a, sqrt(n));
   return a;
 }
 DT_HD double dmin(double a, double b) { return (b < a) ? b : a; }   // std::min

@@ -118,6 +118,8 @@ class FrameQueue:
     frames: the frame ids to render; cost: {frame id: estimated cost} (missing ids: the mean);
     store: a torch.distributed Store (None: a single process, plain iteration)."""
 
+    _instances = 0   # queues made in this process: every rank makes them in the same sequence
+
     def __init__(self, frames, cost=None, store=None, key="dt_frame_queue"):
         cost = cost or {}
         known = [cost[n] for n in frames if n in cost]
@@ -125,8 +127,21 @@ class FrameQueue:
         # stable: equal costs keep the frames' own order
         self.order = sorted(frames, key=lambda n: -cost.get(n, mean))
         self.store = store
-        self.key = key
+        # a fresh counter per queue (a second pass or a retry in the same process group starts at
+        # 0, not past the end of the previous queue's counter)
+        self.key = "%s/%d" % (key, FrameQueue._instances)
+        FrameQueue._instances += 1
         self._local = 0
+        if store is not None:
+            # every rank must hand out the same order, or frames would be rendered twice or never:
+            # the first rank stores a hash of its order, the others must find the same one
+            import hashlib
+            h = hashlib.sha1(repr(self.order).encode()).hexdigest()
+            got = store.compare_set(self.key + "/order", "", h)
+            got = got.decode() if isinstance(got, bytes) else got
+            if got != h:
+                raise RuntimeError("FrameQueue %s: this rank's frame order differs from another rank's "
+                                   "(different frame lists or cost data)" % self.key)
 
     def next(self):
         """the next frame id, or None when every frame has been handed out"""

@@ -40,7 +40,8 @@ extern "C" {
  *    dt_scene_prepare / dt_scene_upload / dt_accel_info_build, RectPrismWithCylinder
  *    (DT_SHAPE_RECTPRISM_CYL with the dt_scene_desc.holes array) */
 /* 3: dt_stats.donations / donate_overflow (DFS work sharing inside a wave, DT_DONATE) */
-#define DT_ABI_VERSION 3
+/* 4: dt_scene_set_kernel (the trace-kernel choice per scene, not through the environment) */
+#define DT_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------- */
 #define DT_OK              0
@@ -262,6 +263,20 @@ void dt_scene_destroy(dt_scene* s);
 int  dt_scene_prepare(const dt_scene_desc* desc, const dt_globals* g, dt_scene** out);
 int  dt_scene_upload(dt_scene* s);
 
+/* Which trace kernel the renders of scene s launch. No reference counterpart (the reference has
+ * one loop, render_final_project.cpp:1031-1218); every choice renders the same bits.
+ *   DT_KERNEL_AUTO     the DT_DONATE environment variable decides (default: the product kernels)
+ *   DT_KERNEL_PRODUCT  the product kernels (dt_trace_kernel / _w5 by spp)
+ *   DT_KERNEL_DONATE   DFS work sharing inside the wave (dt_trace_kernel_dn) where it applies
+ *                      (max_depth <= 11, brdf_samples <= 6, no RectPrismWithCylinder)
+ * A caller choosing per frame (tools/animate.py) sets it on that frame's scene instead of writing
+ * the process environment while another thread builds the next scene. Calls on one scene must not
+ * overlap across host threads (this one included). */
+#define DT_KERNEL_AUTO     0
+#define DT_KERNEL_PRODUCT  1
+#define DT_KERNEL_DONATE   2
+int  dt_scene_set_kernel(dt_scene* s, int32_t kernel);
+
 /* BVH export for parity tests: node i = {first child or -1, n_children, first shape,
  * n_shapes, leaf, lbound[3], ubound[3]} in the reference's push order. */
 typedef struct dt_bvh_node {
@@ -318,7 +333,11 @@ int dt_debug_normalize(const double* in, double* out, int64_t n);
  * q = r / 8 -> pixel q mod (xRes*yRes) in raster order, sample r mod 8 + 8 * (q div (xRes*yRes)).
  * hit_shape[i], hit_t[i] for ray first_ray + i: the closest shape (-1: none) and its t (FLT_MAX:
  * none); host (out_on_device=0) or device (1) arrays of n_rays. Synchronous; kernel_ms (optional):
- * the kernel's HIP-event time. Scenes with a RectPrismWithCylinder: DT_E_UNSUPPORTED. */
+ * the kernel's HIP-event time. Scenes with a RectPrismWithCylinder: DT_E_UNSUPPORTED. It shares the
+ * scene's primary-ray lists, which depend on the camera and resolution only (not on a tile split):
+ * called with the globals of the scene's renders it rebuilds nothing. Its launch record, counters
+ * and events are its own, but like every call on one scene it must not overlap another call on
+ * that scene from another host thread. */
 int dt_intersect_primary(const dt_scene* s, const dt_globals* g, int32_t frame, int64_t first_ray,
                          int64_t n_rays, int32_t* hit_shape, float* hit_t, int32_t out_on_device,
                          void* stream, float* kernel_ms);

@@ -31,7 +31,7 @@ def test_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert dt.lib.dt_abi_version() == 3 == _lib.ABI_VERSION
+    assert dt.lib.dt_abi_version() == 4 == _lib.ABI_VERSION
 
 
 STRUCTS = {"dt_globals": _lib.Globals, "dt_shape_desc": _lib.ShapeDesc, "dt_light_desc": _lib.LightDesc,
@@ -125,3 +125,10 @@ def test_write_png_matches_ppm_pixels(tmp_path):
     raw = zlib.decompress(data[i + 4:i + 4 + n])
     rows = [raw[r * 10 + 1:(r + 1) * 10] for r in range(2)]
     assert list(b"".join(rows)) == [int(v) for v in vals]
+
+
+def test_scene_set_kernel_null_scene():
+    """dt_scene_set_kernel (ABI 4) rejects a null scene without touching a device (the value
+    checks on a real scene run in tests/test_gpu_donate.py)."""
+    assert dt.lib.dt_scene_set_kernel(None, 0) == -1
+    assert b"null scene" in dt.lib.dt_last_error()

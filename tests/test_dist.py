@@ -120,26 +120,42 @@ def _queue_worker(rank, world, port, result_path):
     try:
         import time
         from distraytracer_amd.multigpu import FrameQueue
+        store = dist.distributed_c10d._get_default_store()
         frames = list(range(0, 40, 2))
         cost = {n: float(n % 7 + (50 if n == 24 else 0)) for n in frames}
-        q = FrameQueue(frames, cost, dist.distributed_c10d._get_default_store())
+        q = FrameQueue(frames, cost, store)
         got = []
         for n in q:
             got.append(n)
             time.sleep(0.002 * cost[n])   # "render": a rank holding a costly frame takes fewer
+        # a second queue in the same process group (a second animation pass) starts afresh
+        q2 = FrameQueue(list(range(5)), None, store)
+        got2 = list(q2)
         everyone = [None] * world
-        dist.all_gather_object(everyone, got)
+        dist.all_gather_object(everyone, [got, got2])
+        # ranks whose cost data disagree must fail loudly, not duplicate or skip frames
+        bad_cost = {n: float(n if rank == 1 else -n) for n in frames}
+        dist.barrier()
+        try:
+            FrameQueue(frames, bad_cost, store)
+            mismatch = False
+        except RuntimeError:
+            mismatch = True
+        flags = [None] * world
+        dist.all_gather_object(flags, mismatch)
         if rank == 0:
             with open(result_path, "w") as f:
                 import json
-                json.dump({"per_rank": everyone, "order": q.order}, f)
+                json.dump({"per_rank": [e[0] for e in everyone], "second": [e[1] for e in everyone],
+                           "order": q.order, "mismatch": flags}, f)
     finally:
         dist.destroy_process_group()
 
 
 def test_frame_queue_hands_out_every_frame_once(tmp_path):
     """C5 frame-parallel (tools/animate.py --split frames): the store counter hands every frame to
-    exactly one rank, most expensive first (LPT); each rank sees its frames in queue order."""
+    exactly one rank, most expensive first (LPT); each rank sees its frames in queue order. A second
+    queue in the same group hands out its frames afresh, and ranks whose frame orders differ raise."""
     import json
     out = str(tmp_path / "q.json")
     mp.start_processes(_queue_worker, args=(3, _free_port(), out), nprocs=3, join=True, start_method="spawn")
@@ -151,6 +167,10 @@ def test_frame_queue_hands_out_every_frame_once(tmp_path):
     for lst in r["per_rank"]:
         pos = [order.index(n) for n in lst]
         assert pos == sorted(pos)
+    assert sorted(n for lst in r["second"] for n in lst) == list(range(5))
+    # rank 1's order is the reverse of ranks 0 and 2's: whichever stored its hash first, the
+    # queue's ranks disagree and at least one of them raised
+    assert any(r["mismatch"])
 
 
 def test_frame_queue_single_process():

@@ -14,8 +14,8 @@ configurations themselves:
 
 Shares are the multi-GPU tile split's own (rank 0 of `world`, slab layout), so they also run the
 slab store path bench.py and multigpu.py use at N > 1. Tolerance (north_star): 1e-4 per
-channel; the images are bit-identical today (max|diff| = 0), the bound on the fraction of
-channels above 1e-4 is the same insurance as in test_gpu_parity.py.
+channel, asserted on the largest channel difference (tests/parity_check.py); the images are
+bit-identical today (max|diff| = 0, logged per case).
 Oracle time on the GPU box's 16 host threads: C3 ~20 s, the others 1-4 s each.
 """
 import numpy as np
@@ -27,7 +27,7 @@ import oracle
 
 pytestmark = pytest.mark.gpu
 
-TOL = 1e-4
+from parity_check import assert_parity
 
 
 def _globals(builder, frame, models, W, H, spp, depth, brdf=2):
@@ -41,7 +41,7 @@ def _globals(builder, frame, models, W, H, spp, depth, brdf=2):
     return g, built
 
 
-def _check(label, g, built, frame, tile, max_bad_frac):
+def _check(label, g, built, frame, tile):
     scene = dt.Scene(built, g)
     if tile.layout == dt.DT_OUT_SLAB:
         n = dt.slab_floats(g, tile)
@@ -52,10 +52,7 @@ def _check(label, g, built, frame, tile, max_bad_frac):
     scene.close()
     gpu = out.cpu().numpy()
     ref, rst = oracle.render(built, g, frame, tile, out=np.zeros(n, dtype=np.float32))
-    diff = np.abs(gpu.astype(np.float64) - ref.astype(np.float64))
-    bad = diff > TOL
-    print("%s: pixels=%d samples=%d rays=%d max|diff|=%.3g channels>1e-4: %d (%.6f)"
-          % (label, st.pixels, st.samples, st.rays, float(diff.max()), int(bad.sum()), float(bad.mean())))
+    print("%s: pixels=%d samples=%d rays=%d" % (label, st.pixels, st.samples, st.rays))
     # identical work: the same rays and shadow rays as the reference loop restated by the oracle
     assert st.pixels == rst.pixels and st.samples == rst.samples
     assert st.rays == rst.rays and st.shadow_rays == rst.shadow_rays
@@ -63,21 +60,21 @@ def _check(label, g, built, frame, tile, max_bad_frac):
     assert st.stack_overflows == 0 and st.nan_pixels == rst.nan_pixels == 0
     assert st.uv_out_of_range == rst.uv_out_of_range
     assert st.glossy_exhausted == rst.glossy_exhausted
-    assert float(bad.mean()) <= max_bad_frac, "%s: %.6f of channels differ by > %g" % (label, bad.mean(), TOL)
+    assert_parity(label, gpu, ref)
     return st
 
 
 def test_c3_full_frame(cuda):
     """C3, the whole 1920x1080 frame at 64 spp, depth 8 (BASELINE.json configs[2])."""
     g, built = _globals("final", 240, 0, 1920, 1080, 64, 8)
-    st = _check("C3 full frame", g, built, 240, dt.tiles(), 1e-4)
+    st = _check("C3 full frame", g, built, 240, dt.tiles())
     assert st.samples == 1920 * 1080 * 64
 
 
 def test_c2_full_frame(cuda):
     """C2, the whole 800x600 frame at 16 spp, depth 4 (BASELINE.json configs[1])."""
     g, built = _globals("final", 240, 0, 800, 600, 16, 4)
-    st = _check("C2 full frame", g, built, 240, dt.tiles(), 1e-4)
+    st = _check("C2 full frame", g, built, 240, dt.tiles())
     assert st.samples == 800 * 600 * 16
 
 
@@ -87,7 +84,7 @@ def test_c4_256spp_share(cuda):
     frame, the model columns included)."""
     g, built = _globals("final", 240, 1, 1920, 1080, 256, 8)
     tile = dt.tiles(rank=0, world=64, layout=dt.DT_OUT_SLAB)
-    st = _check("C4 256 spp 1/64", g, built, 240, tile, 1e-4)
+    st = _check("C4 256 spp 1/64", g, built, 240, tile)
     assert st.samples == st.pixels * 256 and st.tex_fetches > 0
 
 
@@ -109,7 +106,7 @@ def test_c5_4k_frame_share(cuda, n, what):
     if not cloud:
         assert g.antialias_samples == 64 and g.max_depth == 10
     tile = dt.tiles(rank=0, world=512, layout=dt.DT_OUT_SLAB)
-    st = _check("C5 frame %d (%s) 1/512" % (n * 8, what), g, built, n * 8, tile, 3e-4)
+    st = _check("C5 frame %d (%s) 1/512" % (n * 8, what), g, built, n * 8, tile)
     if cloud:
         assert st.samples == st.pixels and st.sky_pixels > 0
     else:

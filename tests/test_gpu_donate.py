@@ -13,14 +13,19 @@ import torch
 
 import distraytracer_amd as dt
 import oracle
+from parity_check import assert_parity, log_equal
 from test_gpu_configs import _globals
 
 pytestmark = pytest.mark.gpu
 
 
-def _render(g, built, frame, tile, donate, monkeypatch):
-    monkeypatch.setenv("DT_DONATE", "1" if donate else "0")
+def _render(g, built, frame, tile, donate, monkeypatch, via_env=False):
+    """donate through dt_scene_set_kernel (the scene's own choice), or via_env: DT_KERNEL_AUTO and
+    the DT_DONATE environment variable"""
+    monkeypatch.setenv("DT_DONATE", "1" if donate and via_env else "0")
     scene = dt.Scene(built, g)
+    if not via_env:
+        scene.set_kernel(dt.DT_KERNEL_DONATE if donate else dt.DT_KERNEL_PRODUCT)
     n = dt.slab_floats(g, tile) if tile.layout == dt.DT_OUT_SLAB else 3 * g.xRes * g.yRes
     out = torch.zeros(n, dtype=torch.float32, device="cuda")
     st = dt.render(scene, g, frame, out, tile)
@@ -48,11 +53,22 @@ def test_donate_bit_identical(cuda, monkeypatch, case):
     assert st0.donations == 0
     assert st.donate_overflow == 0 and st.stack_overflows == 0
     assert st.rays == st0.rays and st.shadow_rays == st0.shadow_rays and st.samples == st0.samples
-    assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), \
-        "%s: %d channels differ" % (label, int((img != base).sum()))
+    log_equal("%s work-sharing kernel vs product kernel (bits)" % label, img.view(np.uint32), base.view(np.uint32))
     if donates:
         assert st.donations > 0   # the deep cascades did donate
+        img_env, st_env = _render(g, built, frame, tile, True, monkeypatch, via_env=True)
+        assert st_env.donations > 0
+        log_equal("%s work-sharing kernel via DT_DONATE (bits)" % label, img_env.view(np.uint32), base.view(np.uint32))
     if check_oracle:
         ref, rst = oracle.render(built, g, frame, tile, out=np.zeros(img.size, dtype=np.float32))
         assert st.rays == rst.rays
-        assert float(np.abs(img.astype(np.float64) - ref.astype(np.float64)).max()) <= 1e-4
+        assert_parity("%s work-sharing kernel vs oracle" % label, img, ref)
+
+
+def test_set_kernel_rejects_unknown_choice(cuda):
+    g, built = _globals("final", 240, 0, 64, 32, 4, 2)
+    scene = dt.Scene(built, g)
+    for k in (dt.DT_KERNEL_AUTO, dt.DT_KERNEL_PRODUCT, dt.DT_KERNEL_DONATE):
+        scene.set_kernel(k)
+    assert dt.lib.dt_scene_set_kernel(scene.handle, 7) == -1
+    scene.close()

@@ -133,15 +133,17 @@ def main():
     donated = 0
 
     def choose_kernel(scene, g, n):
-        """DT_DONATE for frame n's render: the probe's rays per sample decide (--donate auto)"""
+        """the trace kernel of frame n's scene (dt_scene_set_kernel, never the process environment:
+        the worker thread is building the next scene meanwhile): the probe's rays per sample decide
+        (--donate auto)"""
         if args.donate != "auto":
-            os.environ["DT_DONATE"] = "1" if args.donate == "on" else "0"
+            scene.set_kernel(dt.DT_KERNEL_DONATE if args.donate == "on" else dt.DT_KERNEL_PRODUCT)
             return args.donate == "on", None
-        os.environ["DT_DONATE"] = "0"
+        scene.set_kernel(dt.DT_KERNEL_PRODUCT)
         pst = dt.render(scene, g, n * 8, probe, probe_tile)
         rps = pst.rays / max(pst.samples, 1)
         on = rps > args.donate_rps
-        os.environ["DT_DONATE"] = "1" if on else "0"
+        scene.set_kernel(dt.DT_KERNEL_DONATE if on else dt.DT_KERNEL_PRODUCT)
         return on, rps
     # frame n+1's host build runs on a worker thread while frame n renders (ctypes releases the
     # GIL inside the library calls)
