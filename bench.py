@@ -48,7 +48,7 @@ def _cpu_model():
     return None
 
 
-def cpu_baseline(dt, cfg, frac_world, scene, dev):
+def cpu_baseline(dt, cfg, frac_world, scene, dev, all_cores=False):
     """The CPU oracle (the reference loop restated in C, same RNG) on a bounded, spatially uniform
     sample of the same frame: rank 0's share of a `frac_world`-way tile split. SURVEY §8(d): the
     host's cores (OpenMP dynamic), median of 3 after 1 warm-up, plus 1 core. The GPU renders the
@@ -101,7 +101,25 @@ def cpu_baseline(dt, cfg, frac_world, scene, dev):
                      % (threads, frac_world, st.pixels, st.samples // max(st.pixels, 1),
                         "/".join("%.2f" % t for t in times)),
            "single_core": {"value": round(st1.samples / dt1 / 1e6, 4), "cores": 1,
-                           "sample": "rank 0's share of a %d-way split, %.1f s" % (frac_world * 16, dt1)}}
+                           "sample": "rank 0's share of a %d-way split, %.1f s" % (frac_world * 16, dt1),
+                           "note": "like for like with the reference, whose render loop is single-threaded "
+                                   "(render_final_project.cpp:1031-1218)"}}
+    if all_cores and affinity > threads:
+        # every core of the affinity mask; off by default on the GPU box, whose pool
+        # rules give one GPU's job a 16-core share of the node (OMP_NUM_THREADS) even though the
+        # affinity mask shows all of the node's cores
+        ta = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            _, sta = oracle.render(built, g, 240, tile, out=out, nthreads=affinity)
+            ta.append(time.perf_counter() - t0)
+        cpu["all_cores"] = {"value": round(sta.samples / statistics.median(ta) / 1e6, 4), "cores": affinity,
+                            "sample": "same share, median of 3: %s s" % "/".join("%.2f" % t for t in ta)}
+    else:
+        cpu["all_cores"] = {"measured": False, "cores": affinity,
+                            "reason": "the job's CPU share is OMP_NUM_THREADS=%s of the %d cores in the affinity "
+                                      "mask; bench.py --cpu-all-cores times every core" % (omp or None, affinity)
+                            if affinity > threads else "the threads above are every core of the affinity mask"}
     return cpu, parity, work, st.samples
 
 
@@ -125,11 +143,34 @@ def end_to_end_ms(dt, cfg, dev):
     return round(sorted(times)[1] * 1e3, 3)
 
 
-def valu_roofline(cfg, kernel_ms, samples, ref_work=None, ref_samples=0):
+def counter_fp64(pmc, kernel_ms):
+    """The FP64 rate the PMC counters give for the trace kernel: the committed
+    profile's FP64 VALU instructions per launch (ADD + MUL + TRANS + 2 FMA, wave instructions) x 64
+    lanes x the VALU lane utilisation, / this run's kernel time. A cross-check of the dt_work.h weight
+    table: the two rates are computed from independent data (event counts x weights, hardware
+    counters) and should agree."""
+    f = (pmc or {}).get("f64_insts_per_launch") or {}
+    lanes = (pmc or {}).get("valu_lane_utilisation")
+    if not f or not lanes or not kernel_ms:
+        return None
+    insts = f.get("add", 0) + f.get("mul", 0) + f.get("trans", 0) + 2 * f.get("fma", 0)
+    flops = insts * 64 * lanes
+    from distraytracer_amd import work as W
+    r = {"achieved": round(flops / (kernel_ms / 1e3) / 1e12, 4), "unit": "TFLOP/s",
+         "frac": round(flops / (kernel_ms / 1e3) / 1e12 / W.PEAK_FP64_TFLOPS, 5),
+         "flops_per_launch": flops, "profile": "profiles/%s_summary.json" % pmc.get("tag"),
+         "formula": "(SQ_INSTS_VALU_ADD_F64 + MUL_F64 + TRANS_F64 + 2 FMA_F64) x 64 x lane utilisation / kernel_ms"}
+    if pmc.get("valu_insts_per_launch"):
+        r["f64_share_of_valu_insts"] = round((insts - f.get("fma", 0)) / pmc["valu_insts_per_launch"], 4)
+    return r
+
+
+def valu_roofline(cfg, kernel_ms, samples, ref_work=None, ref_samples=0, pmc=None):
     """the binding roofline is the VALU. achieved = the include/dt_work.h events the
     trace kernel executes for this frame (counted by the diagnostic library in a child process) x
-    their weights, / the trace kernel's HIP-event time; against the MI355X FP64 vector peak. The
-    reference loop's count for the same frame (the oracle's, scaled from its sample) beside it."""
+    their weights, / the trace kernel's HIP-event time; against the MI355X FP64 vector peak. Beside
+    it: the counter-derived FP64 rate of the committed PMC profile (counter_fp64) and the reference
+    loop's count for the same frame (the oracle's, scaled from its sample)."""
     from distraytracer_amd import work as W
     dev = W.device_counts(cfg)
     if dev is None:
@@ -142,10 +183,12 @@ def valu_roofline(cfg, kernel_ms, samples, ref_work=None, ref_samples=0):
          "kernel": None, "kernel_ms": round(kernel_ms, 3),   # named by the caller
          "counts_per_sample": W.breakdown(dev["counts"], dev["samples"]),
          "note": "FP64-equivalent VALU operations of the events the kernel executes (include/dt_work.h "
-                 "weights x libdt_work.so counts). Every operation is unfused (no FMA contraction, for "
-                 "parity), while the 78.6 TFLOP/s peak counts an FMA as 2: the ceiling for this code is "
-                 "half of it, frac_unfused_ceiling = 2 frac"}
-    r["frac_unfused_ceiling"] = round(2 * r["frac"], 5)
+                 "weights x libdt_work.so counts) / the trace kernel's HIP-event time, against the "
+                 "78.6 TFLOP/s FP64 vector peak (an FMA counts 2 there and in counter_fp64)"}
+    cf = counter_fp64(pmc, kernel_ms)
+    if cf is not None:
+        cf["ratio_to_weighted"] = round(cf["achieved"] / achieved, 4) if achieved else None
+        r["counter_fp64"] = cf
     if ref_work is not None and ref_samples:
         ref_ops = W.price(ref_work) / ref_samples
         r["reference_loop"] = {"ops_per_sample": round(ref_ops, 2),
@@ -184,6 +227,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frac", type=int, default=8, help="CPU baseline renders 1/N of the tiles")
+    ap.add_argument("--cpu-all-cores", action="store_true",
+                    help="also time the CPU baseline on every core of the affinity mask (not the GPU box's default)")
     ap.add_argument("--no-roofline", action="store_true", help="skip the VALU work count (child process)")
     ap.add_argument("--inflight", type=int, default=2, choices=(1, 2),
                     help="N > 1 (torchrun): frames in flight per rank (2: alternating streams, DESIGN.md §7)")
@@ -301,10 +346,12 @@ def main():
         cpu, parity, ref_work, ref_samples = None, None, None, 0
         e2e = end_to_end_ms(dt, args.config, dev) if world == 1 else None
         if world == 1 and not args.no_cpu_baseline:
-            cpu, parity, ref_work, ref_samples = cpu_baseline(dt, args.config, args.cpu_frac, scene, dev)
+            cpu, parity, ref_work, ref_samples = cpu_baseline(dt, args.config, args.cpu_frac, scene, dev,
+                                                              args.cpu_all_cores)
         roof = None
         if world == 1 and not args.no_roofline:
-            roof = valu_roofline(args.config, kernel_ms, W * H * spp, ref_work, ref_samples)
+            roof = valu_roofline(args.config, kernel_ms, W * H * spp, ref_work, ref_samples,
+                                 pmc if pmc.get("kernel") == trace_kernel_name(spp) else None)
         if roof is not None:
             roof["kernel"] = trace_kernel_name(spp)
         if roof is None:   # no diagnostic library (or N > 1): the HBM line alone

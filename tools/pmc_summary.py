@@ -12,7 +12,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(tag, kernel="dt_trace_kernel"):
+def main(tag, kernel="dt_trace_kernel", config="c3"):
     src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
     acc = collections.defaultdict(float)
     n_disp = collections.defaultdict(int)
@@ -58,10 +58,17 @@ def main(tag, kernel="dt_trace_kernel"):
         shutil.copy(stats, os.path.join(ROOT, "profiles", "%s_kernel_stats.csv" % tag))
     # the profile bench.py's roofline.traffic reads (the latest summarised tag)
     with open(os.path.join(ROOT, "profiles", "pmc_trace_summary.json"), "w") as fh:
-        json.dump({k: out.get(k) for k in ("tag", "kernel", "avg_duration_ns", "hbm_bytes_per_launch",
-                                            "valu_active_per_wave_cycle", "valu_lane_utilisation", "waves_per_simd",
-                                            "fp64_tflops_upper")},
-                  fh, indent=1, sort_keys=True)
+        d = {k: out.get(k) for k in ("tag", "kernel", "avg_duration_ns", "hbm_bytes_per_launch",
+                                     "valu_active_per_wave_cycle", "valu_lane_utilisation", "waves_per_simd",
+                                     "fp64_tflops_upper")}
+        # the FP64 VALU instruction counts per launch: bench.py's counter-derived FP64 rate
+        d["f64_insts_per_launch"] = {k: per[c] for k, c in (("add", "SQ_INSTS_VALU_ADD_F64"),
+                                                             ("mul", "SQ_INSTS_VALU_MUL_F64"),
+                                                             ("fma", "SQ_INSTS_VALU_FMA_F64"),
+                                                             ("trans", "SQ_INSTS_VALU_TRANS_F64")) if c in per}
+        d["valu_insts_per_launch"] = per.get("SQ_INSTS_VALU")
+        d["config"] = config
+        json.dump(d, fh, indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
     return out
 
