@@ -109,6 +109,9 @@ using namespace dtd;
 #define DT_PSUM_LDS 1   // per-pixel sums in LDS: 1 for up to 64 pixels per wave, 2 for up to 8 (DT_W5)
 #endif
 #define DT_LS_CACHE 4   // area lights whose sample pair is kept in LDS between the two light passes
+#ifndef DT_ONEPASS
+#define DT_ONEPASS 0    // 1: one pass over the lights, each BRDF right after its shadow walk (run_pass)
+#endif
 
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
        ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15,
@@ -1166,7 +1169,8 @@ __device__ __forceinline__ bool box_hit_exact_finite(const DNodeDev& b, const Ra
 // padding), so a culled box holds no hit the reference would have used: the result is
 // unchanged, only the gather is smaller. Callers pass FLT_MAX to disable it.
 // (Measured slower and dropped: an f32 pre-test with an exact fallback, 1515 vs 1606 Msps on C3;
-// wave-uniform slab-end selection for sign-coherent waves, 1482 vs 1630.)
+// wave-uniform slab-end selection for sign-coherent waves, 1482 vs 1630; again in round 4 with the
+// selection on the scalar unit: VALU +1.9%, SALU +10%, C3 -2.4%, C4 -7%, profiles/r04b_ab.log.)
 __device__ __forceinline__ bool box_hit_finite(const DNodeDev& b, const RayBox& r, V3 st, float tcull)
 {
   return box_hit_exact_finite(b, r, st, tcull);
@@ -1568,10 +1572,13 @@ __device__ bool occluded_list(const DScene& S, const Walk& w, bool active, V3 bs
 // Every lane must be enabled in exec (the callers run at wave-uniform control flow).
 __device__ __forceinline__ int wave_min_u(int v)
 {
-  v = min(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));    // quad_perm [1,0,3,2]
-  v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
-  v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));   // row_half_mirror
-  v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));   // row_mirror
+  // bound_ctrl set: every source lane of these row permutations is valid, so it changes nothing, but
+  // it lets the compiler fold each move into the min (v_min_i32_dpp: 4 VALU instead of 12; VALU
+  // -0.9%, C3 +0.2%, C4 +0.8%, profiles/r04b_ab.log)
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true));    // quad_perm [1,0,3,2]
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true));    // quad_perm [2,3,0,1]
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true));   // row_half_mirror
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true));   // row_mirror
   const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
   const int c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
   return min(min(a, b), min(c, d));
@@ -1865,6 +1872,59 @@ __device__ __forceinline__ float schlick_complex(float cos_theta, float R0)
   return (float)((R0 + (1 - R0)) + pw5((double)(1 - cos_theta)));
 }
 
+// the light's BRDF at a hit (cpp:894-948): Oren-Nayar, Cook-Torrance, raw or Phong
+__device__ __forceinline__ V3 brdf(const DParams& P, const DMat& M, const DT_CAS DLight& L, V3 normal, V3 e_dir,
+                                   V3 sray, V3 sn, V3 shape_color)
+{
+  V3 lc = v3a(L.color);
+  V3 ray_col;
+  const float roughness = M.roughness;
+  if (M.model == DT_MODEL_OREN_NAYAR) {
+    const float A = M.on_a, B = M.on_b;   // per material (host, cpp:896-897)
+    float vn = (float)dot(e_dir, normal);
+    float ln = (float)dot(sn, normal);
+    float irradiance = fmaxr(0.0f, ln);
+    float vn_theta = cr_acosf(vn), ln_theta = cr_acosf(ln);
+    float angleDiff = (float)dmax(0.0, dot(normalized(sub(e_dir, mul(vn, normal))),
+                                           normalized(sub(sray, mul(ln, normal)))));
+    float alpha = fmaxr(vn_theta, ln_theta), beta = fminr(vn_theta, ln_theta);
+    float f = A + B * angleDiff * cr_sinf(alpha) * cr_tanf(beta);
+    ray_col = mul(f, mul(irradiance, cwise(shape_color, lc)));
+  }
+  else if (M.model == DT_MODEL_COOK_TORRANCE) {
+    V3 H = normalized(add(e_dir, sray));
+    float hn = (float)dmax(0.0, dot(normal, H));
+    float vh = (float)dot(e_dir, H);
+    float vn = (float)dot(e_dir, normal);
+    float ln = (float)dot(sn, normal);
+    float alpha = cr_acosf(hn);
+    double sa, ca;
+    cr_sincos_d(alpha, sa, ca);   // cosf(alpha), tanf(alpha) from one reduction
+    const float cos_a = (float)ca, tan_a = (float)(sa / ca);
+    float D = (float)(1 / (pw2((double)roughness) * pw4((double)cos_a)) *
+                      exp(-pw2((double)(tan_a / roughness))));
+    float G1 = (float)(2.0 * hn * vn / vh);
+    float G2 = (float)(2.0 * hn * ln / vh);
+    float G = 1.0f;
+    if (G1 < G) G = G1;
+    if (G2 < G) G = G2;
+    float F = schlick_complex(vn, M.ct_r0);
+    float fdg = F * D * G;
+    double den = (double)(ln * vn) * M_PI;
+    V3 shader_rgb = add(mul(fmaxr(0.0f, ln), mul(0.4, lc)), divs(mul(fdg, mul(0.8, lc)), den));
+    ray_col = cwise(shape_color, shader_rgb);
+  } else if (M.model == DT_MODEL_RAW) {
+    ray_col = shape_color;
+  } else {
+    V3 r = normalized(add(mul(-1, sray), mul(2 * dot(normal, sray), normal)));
+    double m1 = dmax(0.0, dot(normal, sn));
+    double pp = pw_rt(dmax(0.0, dot(r, e_dir)), (double)P.phong);
+    V3 shader_rgb = add(mul(m1, lc), mul(pp, lc));
+    ray_col = cwise(shape_color, shader_rgb);
+  }
+  return ray_col;
+}
+
 // =====================================================================================
 // DFS work sharing (DT_DONATE, dt_trace_kernel_dn)
 // =====================================================================================
@@ -1930,7 +1990,7 @@ __device__ __forceinline__ void dn_put(const DnCtx& dn, int& pos, double x, doub
 // reference's accumulation order.
 __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, V3 org0, uint32_t rootkey, float shift_in,
                          PassOut& out, Entry* stack, Counters& cnt, double (*nrec)[DT_WAVE],
-                         double (*ocol)[DT_WAVE], float (*lsxy)[2][DT_WAVE]
+                         double (*ocol)[DT_WAVE], float (*lsxy)[2][DT_WAVE], double (*tcol)[DT_WAVE]
 #if DT_DONATE
                          , const DnCtx& dn
 #endif
@@ -2373,6 +2433,88 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
       if (textured) uvt = shape_uv(hd.type, hd.flags, cas(S.geom) + hd.off, isectP, shift, tu, tv);
       const bool walk = shade && uvt != 0;
       const int ln_ = threadIdx.x & (DT_WAVE - 1);
+#if DT_ONEPASS
+      // One pass over the lights: each light's BRDF right after its shadow walk, for the lanes the
+      // light reaches, in light order as the reference's loop (cpp:800-959). The walk's sray and sn
+      // serve the BRDF, so the sample is neither kept for nor regenerated in a second pass. Parked
+      // in LDS across the walks: the normal, the eye direction (normalised once per node) and the
+      // base colour; the colour sum of the lit lights in tcol.
+      if (walk) {
+        V3 base = shape_color;
+        if (textured) {
+          const DMat& M = S.mat[sid];
+          if (uvt == 2) {
+            base = v3a(M.bordercolor);
+          } else if (uvt == 1 && M.tex >= 0) {
+            double dims0 = M.tex_w;
+            int x_tex = (int)((float)(M.tex_w - 1) * (float)tu);
+            int y_tex = (int)((float)(M.tex_h - 1) * (float)tv);
+            int uv_ind = (int)(y_tex * dims0 + x_tex);
+            if (uv_ind < 0) uv_ind = 0;
+            if (uv_ind >= M.tex_w * M.tex_h) uv_ind = M.tex_w * M.tex_h - 1;
+            const uint8_t* px = S.tex + M.tex_off + (int64_t)uv_ind * M.tex_ch;
+            base = v3(px[0] / 255.0, px[1] / 255.0, px[2] / 255.0);
+          }
+        }
+        const V3 e_dir = normalized(sub(eye, isectP));
+        nrec[0][ln_] = normal.x; nrec[1][ln_] = normal.y; nrec[2][ln_] = normal.z;
+        nrec[3][ln_] = e_dir.x; nrec[4][ln_] = e_dir.y; nrec[5][ln_] = e_dir.z;
+        nrec[6][ln_] = base.x; nrec[7][ln_] = base.y; nrec[8][ln_] = base.z;
+        tcol[0][ln_] = 0; tcol[1][ln_] = 0; tcol[2][ln_] = 0;
+      }
+      const bool uv_oob = textured && (tu < 0 || tv < 0 || tu > 1 || tv > 1);
+      asm volatile("" ::: "memory");
+      int hits = 0;
+      DT_WORK(bool tex_counted = false);
+      uint32_t pair[3] = {0u, 0u, 0xffffffffu};   // area-light draw shared with the next light
+      for (int li = 0; li < P.n_lights; ++li) {
+        const DT_CAS DLight& L = cas(S.lights)[li];
+        DT_CNT(9);
+        V3 sray = v3(1, 0, 0);
+        float t_max = 0;
+        V3 sn = v3(1, 0, 0);
+        if (walk) {
+          DT_WK(DT_WK_LIGHT, true);
+          sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL, nullptr, 0, pair);
+          t_max = (float)norm(sray);
+          sn = normalized(sray);
+          DT_WCNT(WC_SHADOW, true);
+        }
+        DT_T(t4);
+#ifdef DT_STAMPS
+        cnt.cur_li = li;
+#endif
+        bool occl = occluded(S, P, walk, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
+                             t_max, L.shape_index, li, shift, cnt);
+        DT_T(t5);
+        DT_ACC(3, t4, t5);
+        asm volatile("" ::: "memory");
+        if (walk && !occl) {
+          const DMat& M = S.mat[sid];
+#ifdef DT_WORK_COUNTERS
+          for (int m = 0; m < 4; ++m) DT_WK(DT_WK_BRDF + m, M.model == m);
+#endif
+          const V3 normal = v3(nrec[0][ln_], nrec[1][ln_], nrec[2][ln_]);
+          const V3 e_dir = v3(nrec[3][ln_], nrec[4][ln_], nrec[5][ln_]);
+          const V3 shape_color = v3(nrec[6][ln_], nrec[7][ln_], nrec[8][ln_]);
+          if (textured) {
+            DT_WK(DT_WK_TEX, !tex_counted);   // getUV + texel once per node, as the two-pass count
+            DT_WORK(tex_counted = true);
+            if (uv_oob) atomicAdd(S.stats + ST_UV, 1ull);   // the reference terminates here (Q9)
+            DT_WCNT(WC_TEX, uvt == 1 && M.tex >= 0);
+          }
+          const V3 ray_col = brdf(P, M, cas(S.lights)[li], normal, e_dir, sray, sn, shape_color);
+          if (!is_approx_zero(ray_col)) {
+            hits++;
+            tcol[0][ln_] = tcol[0][ln_] + k * ray_col.x;
+            tcol[1][ln_] = tcol[1][ln_] + k * ray_col.y;
+            tcol[2][ln_] = tcol[2][ln_] + k * ray_col.z;
+          }
+        }
+      }
+      if (hits > 0) own = divs(v3(tcol[0][ln_], tcol[1][ln_], tcol[2][ln_]), hits);
+    }
+#else
       if (walk) {
         nrec[0][ln_] = normal.x; nrec[1][ln_] = normal.y; nrec[2][ln_] = normal.z;
         nrec[3][ln_] = eye.x; nrec[4][ln_] = eye.y; nrec[5][ln_] = eye.z;
@@ -2471,56 +2613,11 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
                                        cache ? 2 : 0);
           const V3 sn = normalized(sray);
           const V3 normal = nrm;
-          V3 lc = v3a(L.color);
           if (textured) {
             if (uv_oob) atomicAdd(S.stats + ST_UV, 1ull);   // the reference terminates here (Q9)
             DT_WCNT(WC_TEX, uvt == 1 && M.tex >= 0);
           }
-          V3 ray_col;
-          const float roughness = M.roughness;
-          if (M.model == DT_MODEL_OREN_NAYAR) {
-            const float A = M.on_a, B = M.on_b;   // per material (host, cpp:896-897)
-            float vn = (float)dot(e_dir, normal);
-            float ln = (float)dot(sn, normal);
-            float irradiance = fmaxr(0.0f, ln);
-            float vn_theta = cr_acosf(vn), ln_theta = cr_acosf(ln);
-            float angleDiff = (float)dmax(0.0, dot(normalized(sub(e_dir, mul(vn, normal))),
-                                                   normalized(sub(sray, mul(ln, normal)))));
-            float alpha = fmaxr(vn_theta, ln_theta), beta = fminr(vn_theta, ln_theta);
-            float f = A + B * angleDiff * cr_sinf(alpha) * cr_tanf(beta);
-            ray_col = mul(f, mul(irradiance, cwise(shape_color, lc)));
-          }
-          else if (M.model == DT_MODEL_COOK_TORRANCE) {
-            V3 H = normalized(add(e_dir, sray));
-            float hn = (float)dmax(0.0, dot(normal, H));
-            float vh = (float)dot(e_dir, H);
-            float vn = (float)dot(e_dir, normal);
-            float ln = (float)dot(sn, normal);
-            float alpha = cr_acosf(hn);
-            double sa, ca;
-            cr_sincos_d(alpha, sa, ca);   // cosf(alpha), tanf(alpha) from one reduction
-            const float cos_a = (float)ca, tan_a = (float)(sa / ca);
-            float D = (float)(1 / (pw2((double)roughness) * pw4((double)cos_a)) *
-                              exp(-pw2((double)(tan_a / roughness))));
-            float G1 = (float)(2.0 * hn * vn / vh);
-            float G2 = (float)(2.0 * hn * ln / vh);
-            float G = 1.0f;
-            if (G1 < G) G = G1;
-            if (G2 < G) G = G2;
-            float F = schlick_complex(vn, M.ct_r0);
-            float fdg = F * D * G;
-            double den = (double)(ln * vn) * M_PI;
-            V3 shader_rgb = add(mul(fmaxr(0.0f, ln), mul(0.4, lc)), divs(mul(fdg, mul(0.8, lc)), den));
-            ray_col = cwise(shape_color, shader_rgb);
-          } else if (M.model == DT_MODEL_RAW) {
-            ray_col = shape_color;
-          } else {
-            V3 r = normalized(add(mul(-1, sray), mul(2 * dot(normal, sray), normal)));
-            double m1 = dmax(0.0, dot(normal, sn));
-            double pp = pw_rt(dmax(0.0, dot(r, e_dir)), (double)P.phong);
-            V3 shader_rgb = add(mul(m1, lc), mul(pp, lc));
-            ray_col = cwise(shape_color, shader_rgb);
-          }
+          const V3 ray_col = brdf(P, M, L, normal, e_dir, sray, sn, shape_color);
           if (!is_approx_zero(ray_col)) {
             hits++;
             tmp_color = add(tmp_color, mul(k, ray_col));
@@ -2529,6 +2626,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
         if (hits > 0) own = divs(tmp_color, hits);
       }
     }
+#endif
     DT_T(t6);
     DT_ACC(4, t3, t6);
     if (fin_slot >= 0) {
@@ -2687,7 +2785,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   // (inside run_pass only); red (per-chunk sample colours) and dens (cloud march chunk) are
   // used after the passes, so they share its space. ocol: the DFS colour accumulator,
   // psum: the per-pixel sums, parked here instead of in registers across the DFS.
-  __shared__ double nrec[DT_NREC_CCOL ? 7 : 9][DT_WAVE];
+  __shared__ double nrec[(DT_NREC_CCOL && !DT_ONEPASS) ? 7 : 9][DT_WAVE];
   double* const red = &nrec[0][0];                        // DT_WAVE * 3 doubles
   float* const dens = (float*)(&nrec[0][0] + DT_WAVE * 3);  // DT_CLOUD_CHUNK floats
   __shared__ double ocol[3][DT_WAVE];
@@ -2696,7 +2794,8 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   __shared__ double psum[3][DT_PSUM_LDS == 2 ? 8 : DT_WAVE];
 #endif
   __shared__ double chan[4];
-  __shared__ float lsxy[DT_LS_CACHE > 0 ? DT_LS_CACHE : 1][2][DT_WAVE];
+  __shared__ float lsxy[(DT_LS_CACHE > 0 && !DT_ONEPASS) ? DT_LS_CACHE : 1][2][DT_WAVE];
+  __shared__ double tcol[DT_ONEPASS ? 3 : 1][DT_WAVE];   // DT_ONEPASS: the lit lights' colour sum
   __shared__ unsigned long long item_s;
   Entry stack[DT_STACK_MAX];
   const int lane = threadIdx.x;
@@ -2810,7 +2909,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         ocol[0][lane] = 0; ocol[1][lane] = 0; ocol[2][lane] = 0;
         po.hit = pass > 0;
         po.in_motion = false;
-        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt, nrec, ocol, lsxy
+        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt, nrec, ocol, lsxy, tcol
 #if DT_DONATE
                  , dn
 #endif
