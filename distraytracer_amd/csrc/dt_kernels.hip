@@ -80,7 +80,7 @@ using namespace dtd;
 #define DT_ISECT 0
 #endif
 // DT_W5=1 (build/dt_kernels_w5.o): the trace kernel at 5 waves per SIMD (96 VGPRs, under 8 KiB of
-// LDS per wave: DT_NREC_CCOL=1, DT_PSUM_LDS=2), launched for one-pixel-per-wave work (spp >= 64; never
+// LDS per wave: DT_PSUM_LDS=2), launched for one-pixel-per-wave work (spp >= 64; never
 // with more than 8 pixels per wave, the slots DT_PSUM_LDS=2 keeps)
 #ifndef DT_W5
 #define DT_W5 0
@@ -102,15 +102,8 @@ using namespace dtd;
 // Measured-and-dropped variants are not kept here (DESIGN.md §8 lists them with their A/B logs;
 // git history holds their code). The switches left select the four instantiations (Makefile).
 #define DT_PRIO_LEVEL 3    // issue priority of long DFS items (P.prio_steps, dt_api.cpp)
-#ifndef DT_NREC_CCOL
-#define DT_NREC_CCOL 0  // the shading record keeps the hit's colour offset, not its colour (1024 B less LDS)
-#endif
 #ifndef DT_PSUM_LDS
 #define DT_PSUM_LDS 1   // per-pixel sums in LDS: 1 for up to 64 pixels per wave, 2 for up to 8 (DT_W5)
-#endif
-#define DT_LS_CACHE 4   // area lights whose sample pair is kept in LDS between the two light passes
-#ifndef DT_ONEPASS
-#define DT_ONEPASS 1    // one pass over the lights, each BRDF right after its shadow walk (run_pass): C3 +4.7%
 #endif
 
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
@@ -1902,39 +1895,27 @@ __device__ __forceinline__ V3 sphere_light_sample(const Ctx& c, const DT_CAS DLi
 }
 
 // light sampleRay (geometry.cpp:2751-2849)
-// xy: the area-light sample's float pair (rect_sample's (float)U draws). cache_mode 1 stores the
-// drawn pair there, 2 reuses the stored pair instead of drawing it again (same values).
 // Area lights 2k and 2k+1 share one draw (sub-index k): words 0-1 are light 2k's (x, y), words
-// 2-3 light 2k+1's. `pair` (pass 1) keeps words 2-3 of an even light's draw,
-// with pair[2] = the odd light they belong to, so the odd light does not draw again.
+// 2-3 light 2k+1's. `pair` keeps words 2-3 of an even light's draw, with
+// pair[2] = the odd light they belong to, so the odd light does not draw again.
 __device__ __forceinline__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L, int li, V3 point, uint32_t node,
-                                           unsigned long long* st_sphl, float* xy = nullptr, int cache_mode = 0,
-                                           uint32_t* pair = nullptr)
+                                           unsigned long long* st_sphl, uint32_t* pair = nullptr)
 {
   if (L.type == DT_LIGHT_POINT) return sub(v3a(L.center), point);
   if (L.type == DT_LIGHT_RECT) {
-    float x, y;
-    if (cache_mode == 2) {
-      x = xy[0];
-      y = xy[DT_WAVE];
+    const bool odd = (li & 1) != 0;
+    uint32_t w0, w1;
+    if (odd && pair && pair[2] == (uint32_t)li) {
+      w0 = pair[0];
+      w1 = pair[1];
     } else {
-      const bool odd = (li & 1) != 0;
-      uint32_t w0, w1;
-      if (odd && pair && pair[2] == (uint32_t)li) {
-        w0 = pair[0];
-        w1 = pair[1];
-      } else {
-        uint32_t o[4];
-        c.rng.draw_words(node, P_LIGHT, (uint32_t)li >> 1, o);
-        w0 = odd ? o[2] : o[0];
-        w1 = odd ? o[3] : o[1];
-        if (pair && !odd) { pair[0] = o[2]; pair[1] = o[3]; pair[2] = (uint32_t)li + 1u; }
-      }
-      x = f01(w0);
-      y = f01(w1);
-      if (cache_mode == 1) { xy[0] = x; xy[DT_WAVE] = y; }
+      uint32_t o[4];
+      c.rng.draw_words(node, P_LIGHT, (uint32_t)li >> 1, o);
+      w0 = odd ? o[2] : o[0];
+      w1 = odd ? o[3] : o[1];
+      if (pair && !odd) { pair[0] = o[2]; pair[1] = o[3]; pair[2] = (uint32_t)li + 1u; }
     }
-    return sub(rect_sample_f(v3a(L.A), v3a(L.B), v3a(L.D), x, y), point);
+    return sub(rect_sample_f(v3a(L.A), v3a(L.B), v3a(L.D), f01(w0), f01(w1)), point);
   }
   return sphere_light_sample(c, L, li, point, node, st_sphl);
 }
@@ -2064,7 +2045,7 @@ __device__ __forceinline__ void dn_put(const DnCtx& dn, int& pos, double x, doub
 // reference's accumulation order.
 __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, V3 org0, uint32_t rootkey, float shift_in,
                          PassOut& out, Entry* stack, Counters& cnt, double (*nrec)[DT_WAVE],
-                         double (*ocol)[DT_WAVE], float (*lsxy)[2][DT_WAVE], double (*tcol)[DT_WAVE]
+                         double (*ocol)[DT_WAVE], double (*tcol)[DT_WAVE]
 #if DT_DONATE
                          , const DnCtx& dn
 #endif
@@ -2507,12 +2488,13 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
       if (textured) uvt = shape_uv(hd.type, hd.flags, cas(S.geom) + hd.off, isectP, shift, tu, tv);
       const bool walk = shade && uvt != 0;
       const int ln_ = threadIdx.x & (DT_WAVE - 1);
-#if DT_ONEPASS
       // One pass over the lights: each light's BRDF right after its shadow walk, for the lanes the
       // light reaches, in light order as the reference's loop (cpp:800-959). The walk's sray and sn
       // serve the BRDF, so the sample is neither kept for nor regenerated in a second pass. Parked
       // in LDS across the walks: the normal, the eye direction (normalised once per node) and the
-      // base colour; the colour sum of the lit lights in tcol.
+      // base colour; the colour sum of the lit lights in tcol. (Round 3 walked every light first and
+      // then evaluated the BRDFs in a second pass, regenerating each sample: C3 -4.8%, C2 -4.6%,
+      // 62 more spilled VGPRs in the 5-wave kernel, profiles/r04e_ab_onepass_all.log.)
       if (walk) {
         V3 base = shape_color;
         if (textured) {
@@ -2549,7 +2531,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
         V3 sn = v3(1, 0, 0);
         if (walk) {
           DT_WK(DT_WK_LIGHT, true);
-          sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL, nullptr, 0, pair);
+          sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL, pair);
           t_max = (float)norm(sray);
           sn = normalized(sray);
           DT_WCNT(WC_SHADOW, true);
@@ -2562,6 +2544,18 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
                              t_max, L.shape_index, li, shift, cnt);
         DT_T(t5);
         DT_ACC(3, t4, t5);
+#ifdef DT_STAMPS
+        {   // per light: (waves, active lanes, occluded lanes), (cycles)
+          const unsigned long long bw = __ballot(walk), bo = __ballot(walk && occl);
+          if ((threadIdx.x & 63) == 0 && li < 8) {
+            unsigned long long* h = S.stats + ST_N + 1 + 64 + 3 * (li * 256 + 255);
+            atomicAdd(h, 1ull);
+            atomicAdd(h + 1, (unsigned long long)__popcll(bw));
+            atomicAdd(h + 2, (unsigned long long)__popcll(bo));
+            atomicAdd(h - 3, (unsigned long long)(t5 - t4));
+          }
+        }
+#endif
         asm volatile("" ::: "memory");
         if (walk && !occl) {
           const DMat& M = S.mat[sid];
@@ -2588,119 +2582,6 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
       }
       if (hits > 0) own = divs(v3(tcol[0][ln_], tcol[1][ln_], tcol[2][ln_]), hits);
     }
-#else
-      if (walk) {
-        nrec[0][ln_] = normal.x; nrec[1][ln_] = normal.y; nrec[2][ln_] = normal.z;
-        nrec[3][ln_] = eye.x; nrec[4][ln_] = eye.y; nrec[5][ln_] = eye.z;
-#if DT_NREC_CCOL
-        ((int*)&nrec[6][0])[ln_] = h.ccol;   // the colour is re-read from its record in pass 2
-#else
-        nrec[6][ln_] = shape_color.x; nrec[7][ln_] = shape_color.y; nrec[8][ln_] = shape_color.z;
-#endif
-      }
-      asm volatile("" ::: "memory");
-      uint32_t vis = 0;
-      uint32_t pair[3] = {0u, 0u, 0xffffffffu};   // area-light draw shared with the next light
-      for (int li = 0; li < P.n_lights; ++li) {
-        const DT_CAS DLight& L = cas(S.lights)[li];
-        DT_CNT(9);
-        V3 sray = v3(1, 0, 0);
-        float t_max = 0;
-        V3 sn = v3(1, 0, 0);
-        if (walk) {
-          DT_WK(DT_WK_LIGHT, true);
-          // the first DT_LS_CACHE area lights park their sample pair in LDS for pass 2
-          const int slot = li - P.ls_first;
-          const bool cache = slot >= 0 && slot < DT_LS_CACHE;
-          sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL, cache ? &lsxy[cache ? slot : 0][0][ln_] : nullptr,
-                              cache ? 1 : 0, pair);
-          t_max = (float)norm(sray);
-          sn = normalized(sray);
-          DT_WCNT(WC_SHADOW, true);
-        }
-        DT_T(t4);
-#ifdef DT_STAMPS
-        cnt.cur_li = li;
-#endif
-        bool occl = occluded(S, P, walk, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
-                             t_max, L.shape_index, li, shift, cnt);
-        DT_T(t5);
-        DT_ACC(3, t4, t5);
-#ifdef DT_STAMPS
-        {   // per light: (waves, active lanes, occluded lanes), (cycles)
-          const unsigned long long bw = __ballot(walk), bo = __ballot(walk && occl);
-          if ((threadIdx.x & 63) == 0 && li < 8) {
-            unsigned long long* h = S.stats + ST_N + 1 + 64 + 3 * (li * 256 + 255);
-            atomicAdd(h, 1ull);
-            atomicAdd(h + 1, (unsigned long long)__popcll(bw));
-            atomicAdd(h + 2, (unsigned long long)__popcll(bo));
-            atomicAdd(h - 3, (unsigned long long)(t5 - t4));
-          }
-        }
-#endif
-        if (walk && !occl) vis |= 1u << li;
-      }
-      asm volatile("" ::: "memory");
-      if (__ballot(vis != 0)) {
-        V3 nrm = v3(0, 0, 0), eye2 = v3(0, 0, 0);
-        if (vis != 0) {
-          nrm = v3(nrec[0][ln_], nrec[1][ln_], nrec[2][ln_]);
-          eye2 = v3(nrec[3][ln_], nrec[4][ln_], nrec[5][ln_]);
-#if DT_NREC_CCOL
-          const int cc = ((const int*)&nrec[6][0])[ln_];
-          shape_color = cc >= 0 ? G3(cas(S.geom) + S.hdr[sid].off, cc) : v3a(S.mat[sid].color);
-#else
-          shape_color = v3(nrec[6][ln_], nrec[7][ln_], nrec[8][ln_]);
-#endif
-        }
-        const DMat* Mp = S.mat + sid;
-        const V3 e_dir = normalized(sub(eye2, isectP));
-        const bool uv_oob = textured && (tu < 0 || tv < 0 || tu > 1 || tv > 1);
-        if (vis != 0 && textured) {
-          DT_WK(DT_WK_TEX, true);
-          const DMat& M = *Mp;
-          if (uvt == 2) {
-            shape_color = v3a(M.bordercolor);
-          } else if (uvt == 1 && M.tex >= 0) {
-            double dims0 = M.tex_w;
-            int x_tex = (int)((float)(M.tex_w - 1) * (float)tu);
-            int y_tex = (int)((float)(M.tex_h - 1) * (float)tv);
-            int uv_ind = (int)(y_tex * dims0 + x_tex);
-            if (uv_ind < 0) uv_ind = 0;
-            if (uv_ind >= M.tex_w * M.tex_h) uv_ind = M.tex_w * M.tex_h - 1;
-            const uint8_t* px = S.tex + M.tex_off + (int64_t)uv_ind * M.tex_ch;
-            shape_color = v3(px[0] / 255.0, px[1] / 255.0, px[2] / 255.0);
-          }
-        }
-        int hits = 0;
-        V3 tmp_color = v3(0, 0, 0);
-        for (int li = 0; li < P.n_lights; ++li) {
-          if (!(vis & (1u << li))) continue;
-          const DT_CAS DLight& L = cas(S.lights)[li];
-          const DMat& M = *Mp;
-#ifdef DT_WORK_COUNTERS
-          for (int m = 0; m < 4; ++m) DT_WK(DT_WK_BRDF + m, M.model == m);
-#endif
-          const int slot = li - P.ls_first;
-          const bool cache = slot >= 0 && slot < DT_LS_CACHE;
-          const V3 sray = light_sample(c, L, li, isectP, node, nullptr, cache ? &lsxy[cache ? slot : 0][0][ln_] : nullptr,
-                                       cache ? 2 : 0);
-          const V3 sn = normalized(sray);
-          const V3 normal = nrm;
-          if (textured) {
-            if (uv_oob) atomicAdd(S.stats + ST_UV, 1ull);   // the reference terminates here (Q9)
-            DT_WCNT(WC_TEX, uvt == 1 && M.tex >= 0);
-          }
-          const V3 ray_col = brdf(P, M, L, normal, e_dir, sray, sn, shape_color);
-          if (!is_approx_zero(ray_col)) {
-            hits++;
-            tmp_color = add(tmp_color, mul(k, ray_col));
-          }
-        }
-        if (hits > 0) own = divs(tmp_color, hits);
-      }
-    }
-#endif
     DT_T(t6);
     DT_ACC(4, t3, t6);
     if (fin_slot >= 0) {
@@ -2859,17 +2740,14 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   // (inside run_pass only); red (per-chunk sample colours) and dens (cloud march chunk) are
   // used after the passes, so they share its space. ocol: the DFS colour accumulator,
   // psum: the per-pixel sums, parked here instead of in registers across the DFS.
-  __shared__ double nrec[(DT_NREC_CCOL && !DT_ONEPASS) ? 7 : 9][DT_WAVE];
+  __shared__ double nrec[9][DT_WAVE];
   double* const red = &nrec[0][0];                        // DT_WAVE * 3 doubles
   float* const dens = (float*)(&nrec[0][0] + DT_WAVE * 3);  // DT_CLOUD_CHUNK floats
   __shared__ double ocol[3][DT_WAVE];
-#if DT_PSUM_LDS
   // DT_PSUM_LDS=2: slots for up to 8 pixels per wave only (spp >= 8; 192 B instead of 1536 B)
   __shared__ double psum[3][DT_PSUM_LDS == 2 ? 8 : DT_WAVE];
-#endif
   __shared__ double chan[4];
-  __shared__ float lsxy[(DT_LS_CACHE > 0 && !DT_ONEPASS) ? DT_LS_CACHE : 1][2][DT_WAVE];
-  __shared__ double tcol[DT_ONEPASS ? 3 : 1][DT_WAVE];   // DT_ONEPASS: the lit lights' colour sum
+  __shared__ double tcol[3][DT_WAVE];   // the lit lights' colour sum of the node being shaded
   __shared__ unsigned long long item_s;
   Entry stack[DT_STACK_MAX];
   const int lane = threadIdx.x;
@@ -2928,13 +2806,9 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     // lanes: pixel slot j = lane / min(spp,64), sample = chunk*64 + lane % ...
     const int per = spp < DT_WAVE ? spp : DT_WAVE;
     const int j = lane / per;
-#if DT_PSUM_LDS
-    if (DT_PSUM_LDS == 1 || lane < 8) {   // lane j (< group): pixel j, sample order
+    if (DT_PSUM_LDS == 1 || lane < 8) {   // pixel j's sums, in sample order
       psum[0][lane] = 0; psum[1][lane] = 0; psum[2][lane] = 0;
     }
-#else
-    V3 psr = v3(0, 0, 0);   // lane j (< group): pixel j's sum, in sample order
-#endif
     int px_x = 0, px_y = 0;
     int64_t px_off = 0;
     bool px_valid = false;
@@ -2983,7 +2857,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         ocol[0][lane] = 0; ocol[1][lane] = 0; ocol[2][lane] = 0;
         po.hit = pass > 0;
         po.in_motion = false;
-        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt, nrec, ocol, lsxy, tcol
+        run_pass(c, act, ray0, eye_sample, root_key(pass), val, po, stack, cnt, nrec, ocol, tcol
 #if DT_DONATE
                  , dn
 #endif
@@ -3036,22 +2910,23 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       red[lane * 3 + 1] = tmp_color.y;
       red[lane * 3 + 2] = tmp_color.z;
       __syncthreads();
-      if (lane < group) {
-        const int base = lane * per;
+      {
         int ns = spp - chunk * DT_WAVE;
         if (ns > per) ns = per;
-        {
-#if DT_PSUM_LDS
+        if (group * 3 <= DT_WAVE) {
+          // lane 3 jj + ch sums channel ch of pixel jj: the three channels' chains run side by side
+          // (the same additions in the same order as one lane adding the three: add() is componentwise)
+          if (lane < group * 3) {
+            const int jj = lane / 3, ch = lane - 3 * jj, base = jj * per;
+            double ps = psum[ch][jj];
+            for (int s = 0; s < ns; ++s) ps = ps + red[(base + s) * 3 + ch];
+            psum[ch][jj] = ps;
+          }
+        } else if (lane < group) {   // (up to 64 pixels per wave: 1 or 2 spp)
+          const int base = lane * per;
           V3 ps = v3(psum[0][lane], psum[1][lane], psum[2][lane]);
-#else
-          V3 ps = psr;
-#endif
           for (int s = 0; s < ns; ++s) ps = add(ps, v3(red[(base + s) * 3], red[(base + s) * 3 + 1], red[(base + s) * 3 + 2]));
-#if DT_PSUM_LDS
           psum[0][lane] = ps.x; psum[1][lane] = ps.y; psum[2][lane] = ps.z;
-#else
-          psr = ps;
-#endif
         }
       }
       __syncthreads();
@@ -3063,11 +2938,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       bool qv;
       pixel_of(P, item * group + lane, qx, qy, qo, qv);
       if (qv && !(P.sky_defer && S.sky_miss[item * group + lane])) {
-#if DT_PSUM_LDS
         V3 color = divs(v3(psum[0][lane], psum[1][lane], psum[2][lane]), spp);
-#else
-        V3 color = divs(psr, spp);
-#endif
 #ifdef DT_ITEM_TIMES   // diagnostic builds (tools/item_times.py): the item's wave cycles / 1e4, raw
         {
           const float cyc = (float)(__builtin_amdgcn_s_memtime() - item_t0) * 1e-4f;
@@ -3255,7 +3126,7 @@ extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_
 extern "C" const void* dt_trace_kernel_ptr(void) { return (const void*)dt_trace_kernel; }
 #elif DT_ISECT
 #elif DT_W5   // the trace kernel at 5 waves per SIMD
-static_assert(DT_TRACE_MIN_WAVES == 5 && DT_NREC_CCOL && DT_PSUM_LDS == 2, "dt_kernels_w5.o: Makefile flags");
+static_assert(DT_TRACE_MIN_WAVES == 5 && DT_PSUM_LDS == 2, "dt_kernels_w5.o: Makefile flags");
 extern "C" hipError_t dt_launch_trace_w5(const void* dev_launch, float* out, int grid, hipStream_t stream)
 {
   hipLaunchKernelGGL(dt_trace_kernel_w5, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);

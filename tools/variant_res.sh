@@ -9,7 +9,7 @@ C=$R/distraytracer_amd/csrc
 name=$1; src=$2; shift 2
 CG="-mllvm -disable-machine-licm -mllvm -disable-machine-cse -mllvm -disable-machine-sink -mllvm -disable-licm-promotion -fno-slp-vectorize -fno-vectorize -mllvm -amdgpu-sched-strategy=max-memory-clause -mllvm -disable-tail-duplicate -mllvm -disable-early-taildup -mllvm -enable-load-pre=false -mllvm -enable-misched=false -fno-unroll-loops -mllvm -structurizecfg-skip-uniform-regions=true"
 case ${KIND:-w5} in
-  w5) KF="-DDT_W5=1 -DDT_TRACE_MIN_WAVES=5 -DDT_NREC_CCOL=1 -DDT_PSUM_LDS=2"; KO=dt_kernels_w5.o; KN=dt_trace_kernel_w5;;
+  w5) KF="-DDT_W5=1 -DDT_TRACE_MIN_WAVES=5 -DDT_PSUM_LDS=2"; KO=dt_kernels_w5.o; KN=dt_trace_kernel_w5;;
   w4) KF="-DDT_TRACE_MIN_WAVES=4"; KO=dt_kernels.o; KN=dt_trace_kernel;;
   dn) KF="-DDT_TRACE_MIN_WAVES=4 -DDT_DONATE=1"; KO=dt_kernels_dn.o; KN=dt_trace_kernel_dn;;
   rpc) KF="-DDT_TRACE_MIN_WAVES=4 -DDT_WITH_RPC=1"; KO=dt_kernels_rpc.o; KN=dt_trace_kernel_rpc;;
