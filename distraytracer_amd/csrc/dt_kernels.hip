@@ -1611,73 +1611,6 @@ __device__ bool occluded_union(const DScene& S, const Walk& w, bool active, V3 b
   return occl;
 }
 
-#ifndef DT_LANE_WALK
-#define DT_LANE_WALK 0
-#endif
-#if DT_LANE_WALK
-// q-th shape of a leaf for this lane (the leaf differs between lanes: vector loads)
-__device__ __forceinline__ void leaf_shape_lane(const DScene& S, const DNodeDev& nd, int q, int& sid, int& type,
-                                                uint32_t& flags, int& off)
-{
-  if (nd.meta & DN_SINGLE) {
-    sid = nd.first;
-    type = (int)((nd.meta >> 4) & 15u);
-    flags = (nd.meta >> 8) & 0xffu;
-    off = nd.aux;
-  } else {
-    sid = S.leaf_idx[nd.first + q];
-    const DShapeHdr hd = S.hdr[sid];
-    type = hd.type;
-    flags = hd.flags;
-    off = hd.off;
-  }
-}
-
-// Scattered waves the shadow grid cannot serve (a lane in a cell whose list is too long: C4's mesh
-// regions) walk the tree lane by lane: each lane follows its own stackless pre-order path (skip
-// links) with vector node loads and tests its own leaves' shapes, instead of the wave walking the
-// union of its lanes' paths on the scalar unit. A lane visits exactly the leaves the wave-uniform
-// walk would test for it (a lane that fails a box fails every box below it: containment and the
-// monotone finite-ray slab test), with the same box and shape tests and the same early exit at an
-// occluder (any-hit), so the result is the same.
-template <class CNT>
-__device__ bool occluded_lane(const DScene& S, const DParams& P, const Walk& w, bool active, V3 bstart, V3 sn,
-                              V3 sstart, float t_max, int skip_shape, CNT& cnt)
-{
-  const bool ftree = P.n_fnodes > 0 && (P.ftree_mode & 2);
-  const DNodeDev* const N = ftree ? S.fnodes : S.nodes;
-  const int n = ftree ? P.n_fnodes : P.n_nodes;
-  const float tcull = shadow_tcull(t_max);
-  bool occl = false;
-  int i = active ? 0 : n;
-  while (__ballot(i < n)) {
-    if (i < n) {
-      const DNodeDev nd = N[i];
-      const bool hb = box_hit_finite(nd, w.rb, bstart, tcull);
-      DT_WK(DT_WK_BOX, true);
-      if (nd.meta & DN_LEAF) {
-        if (hb) {
-          const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
-          for (int q = 0; q < nq && !occl; ++q) {
-            int sid, type, off;
-            uint32_t flags;
-            leaf_shape_lane(S, nd, q, sid, type, flags, off);
-            if (sid != skip_shape) {
-              DT_WK(DT_WK_SHADOW_SHAPE + type, true);
-              if (shape_shadow(type, flags, cas(S.geom) + off, sn, sstart, t_max, 0.0f)) occl = true;
-            }
-          }
-        }
-        i = occl ? n : i + 1;
-      } else {
-        i = hb ? i + 1 : nd.skip;
-      }
-    }
-  }
-  return occl;
-}
-#endif
-
 // shading point in grid-cell coordinates
 __device__ __forceinline__ void sg_coords(const DParams& P, V3 p, float& x, float& y, float& z)
 {
@@ -1706,7 +1639,11 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   // cell lists, merged in leaf order (C3: 4.8 leaves per union against ~24 node visits per tree
   // walk); a wave with a lane outside the grid or in a cell whose list is too long walks the tree.
   // Measured slower for scattered waves: per-lane list walks with a per-lane shape switch (C3 1725
-  // vs 1932, C4 843 vs 936 Mpixel-samples/s), the lists of two cells in turn.
+  // vs 1932, C4 843 vs 936 Mpixel-samples/s), the lists of two cells in turn; round 4, per-lane
+  // stackless tree walks (skip links, vector node loads) for the waves that fall back to the tree:
+  // C3 -18% (register allocation), C4 +0.3%, the C5 transition share +16% (profiles/r04f_ab_lane_walks.log);
+  // the same for scattered closest-hit walks: C3 -8.7%, C4 +3.6%, and +9% on the C5 transition share
+  // in the work-sharing kernel (r04g_ab_uniform_pixel.log). The wave-uniform walk on the scalar unit wins.
   // blur passes use the padded lists, pass-0 rays the unpadded ones when a second grid was built
   const int sg_b = w.bump_wave ? P.sg_base[li] : P.sg_base0[li];
   if (li < P.sg_n && sg_b >= 0) {
@@ -1766,13 +1703,6 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
                          : occluded_union<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
       }
     }
-#if DT_LANE_WALK
-    // scattered waves with a lane in a cell whose list is too long: lane-by-lane tree walks (a
-    // coherent wave in such a cell keeps the wave-uniform walk below)
-    if (!w.bump_wave && !(inside && !__ballot(active & !near))) {
-      return occluded_lane(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, cnt);
-    }
-#endif
   }
 #ifdef DT_STAMPS
   cnt.cur_path = 2;

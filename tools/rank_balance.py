@@ -6,9 +6,8 @@ T_1 / (N * max_r T_r) bounds the kernel-side strong-scaling efficiency of bench.
 
     python tools/rank_balance.py [c3|c2|c4] [reps]     (TILE=<side>: the split's tile side, default 8 as FrameSplit)
 
-INFLIGHT=2: each rank's time per frame over 16 frames rendered back to back on two streams with one
-scene object each, as bench.py renders at N > 1 (two frames in flight), instead of one launch's
-kernel time.
+INFLIGHT=n (2, 3, ...): each rank's time per frame over 16 frames rendered back to back on n streams with
+one scene object each (bench.py renders two in flight at N > 1), instead of one launch's kernel time.
 """
 import json
 import os
@@ -27,21 +26,22 @@ def main():
     g, built = bench.build_globals(dt, cfg)
     scene = dt.Scene(built, g)
     inflight = int(os.environ.get("INFLIGHT", "1"))
-    scene2 = dt.Scene(built, g) if inflight == 2 else None
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    scenes = [scene] + [dt.Scene(built, g) for _ in range(max(inflight, 1) - 1)]
+    streams = [torch.cuda.Stream() for _ in range(max(inflight, 2))]
 
     def frame_ms(tile, out):
-        """wall time per frame of 16 frames on two streams (two frames in flight)"""
+        """wall time per frame of 16 frames on `inflight` streams (frames in flight), one scene each"""
         import time
-        outs = [out, torch.zeros_like(out)]
-        for sc in (scene, scene2):
+        outs = [out] + [torch.zeros_like(out) for _ in range(inflight - 1)]
+        for sc in scenes:
             dt.render(sc, g, 240, out, tile)
         best = None
         for _ in range(reps):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for k in range(16):
-                dt.render_async((scene, scene2)[k % 2], g, 240, outs[k % 2], tile, stream=streams[k % 2].cuda_stream)
+                dt.render_async(scenes[k % inflight], g, 240, outs[k % inflight], tile,
+                                stream=streams[k % inflight].cuda_stream)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) * 1e3 / 16
             best = ms if best is None else min(best, ms)
@@ -54,7 +54,7 @@ def main():
             tile = dt.tiles(rank=rank, world=world, layout=dt.DT_OUT_SLAB, tile_w=ts, tile_h=ts)
             out = torch.zeros(max(dt.slab_floats(g, tile), 1), dtype=torch.float32, device="cuda")
             st = dt.render(scene, g, 240, out, tile)   # warm-up
-            if inflight == 2:
+            if inflight >= 2:
                 best = frame_ms(tile, out)
             else:
                 best = min(dt.render(scene, g, 240, out, tile).kernel_ms for _ in range(reps))
@@ -69,9 +69,8 @@ def main():
         print(json.dumps({"config": cfg, "world": world, "kernel_ms_per_rank": per, "max_ms": mx,
                           "mean_ms": round(sum(per) / world, 3),
                           "kernel_efficiency": round(t1 / (world * mx), 4), "rays_shadow_M": work}), flush=True)
-    scene.close()
-    if scene2 is not None:
-        scene2.close()
+    for sc in scenes:
+        sc.close()
 
 
 if __name__ == "__main__":
