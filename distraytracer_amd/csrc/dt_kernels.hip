@@ -1171,6 +1171,12 @@ __device__ __forceinline__ bool box_hit_finite(const DNodeDev& b, const RayBox& 
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Lane sets of the walks are wave-uniform lane masks (SGPR pairs): a per-lane bool carried through
+// a walk was kept as a 0/1 value in a VGPR and turned back into a mask at every use (up to six VALU
+// instructions per list entry). inv(m): this lane's bit of a uniform mask m, with no VALU
+// (llvm.amdgcn.inverse.ballot: an exec-mask operation).
+__device__ __forceinline__ bool inv(unsigned long long m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+
 __device__ __forceinline__ unsigned long long wave_sum(uint32_t v)
 {
   unsigned long long x = v;
@@ -1212,6 +1218,31 @@ __device__ __forceinline__ bool node_hit(const Walk& w, const DNodeDev& nd, floa
     ub1 = ub1 + shift;
   }
   return box_hit(nd, lb1, ub1, w.rb, st);
+}
+
+// The finite-ray decision of box_hit_exact_finite as the wave's lane mask: the three compares write
+// their masks straight into SGPRs (llvm.amdgcn.fcmp: ordered <=, >, <=, false for NaN as the C
+// compares), so no per-lane bool is materialised and turned back into a mask. Lanes outside exec
+// get no bit, as with a ballot; the callers run at wave-uniform control flow.
+__device__ __forceinline__ unsigned long long box_mask_finite(const DNodeDev& b, const RayBox& r, V3 st, float tcull)
+{
+  const float ax = (float)((b.lb[0] - st.x) * r.inv.x), cx = (float)((b.ub[0] - st.x) * r.inv.x);
+  const float ay = (float)((b.lb[1] - st.y) * r.inv.y), cy = (float)((b.ub[1] - st.y) * r.inv.y);
+  const float az = (float)((b.lb[2] - st.z) * r.inv.z), cz = (float)((b.ub[2] - st.z) * r.inv.z);
+  const float tmin = fmaxf(fmaxf(fminf(ax, cx), fminf(ay, cy)), fminf(az, cz));
+  const float tmax = fminf(fminf(fmaxf(ax, cx), fmaxf(ay, cy)), fmaxf(az, cz));
+  return __builtin_amdgcn_fcmpf(tmin, tmax, 5 /*OLE*/) & __builtin_amdgcn_fcmpf(tmax, 0.0f, 2 /*OGT*/) &
+         __builtin_amdgcn_fcmpf(tmin, tcull, 5 /*OLE*/);
+}
+
+// node_hit as a lane mask: GENERAL waves test lane by lane (act: the lane's own walk state), the
+// finite-ray test runs for the lanes of actm
+template <bool GENERAL>
+__device__ __forceinline__ unsigned long long node_mask(const Walk& w, const DNodeDev& nd, float shift, V3 st,
+                                                        float tcull, unsigned long long actm, bool act)
+{
+  if (GENERAL) return __ballot(act & node_hit<true>(w, nd, shift, st, tcull));
+  return actm & box_mask_finite(nd, w.rb, st, tcull);
 }
 
 // q-th shape of a leaf: (id, type, flags, geom offset), all wave-uniform
@@ -1284,6 +1315,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
   const bool ftree = BUMP || (!GENERAL && P.n_fnodes > 0 && (P.ftree_mode & 1));
   const DNodeDev* const NODES = BUMP ? S.bnodes : ftree ? S.fnodes : S.nodes;
   int resume = active ? 0 : 0x7fffffff;
+  const unsigned long long am = __ballot(active);
   float t_dist = FLT_MAX;
   float tcull = FLT_MAX;   // culling bound from the best hit so far (updated with it)
   bool any = false;
@@ -1300,16 +1332,17 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
     // fast walks need no per-lane resume point: every box contains its subtree's boxes and the
     // finite-ray slab test (with the shrinking tcull) is monotone in the box, so a lane that
     // failed an ancestor fails here too (host_fasttree.cpp)
-    const bool act = GENERAL ? resume <= i : active;
+    const bool act = GENERAL ? resume <= i : inv(am);
     tcull = (h.t_min == FLT_MAX || (DT_WITH_RPC && P.no_cull)) ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
-    bool hb = act & node_hit<GENERAL>(w, nd, shift, org, tcull);
+    unsigned long long hbm = node_mask<GENERAL>(w, nd, shift, org, tcull, am, act);
+    const bool hb = inv(hbm);
     DT_WORK(cnt.wnodes++);
     DT_WK(DT_WK_BOX, act);
     DT_CNT(26);
     if (nd.meta & DN_LEAF) {
       DT_WK(DT_WK_BOX, BUMP && hb);   // the exact bumped gather: the reference leaf's own box test
-      if (BUMP && __ballot(hb)) hb = hb & bump_leaf_gathered(S, w, nd.skip, shift, org);
-      if (__ballot(hb)) {
+      if (BUMP && hbm) hbm = __ballot(hb & bump_leaf_gathered(S, w, nd.skip, shift, org));
+      if (hbm) {
         DT_T(q0);
         const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
         for (int q = 0; q < nq; ++q) {
@@ -1318,7 +1351,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
           leaf_shape(S, nd, q, sid, type, flags, off);
           DT_CNT(8);
           DT_CNT(10 + (type & 7));   // closest-hit prim tests by type (8 -> 10)
-          if (hb) {
+          if (inv(hbm)) {
             DT_WK(DT_WK_HIT_SHAPE + type, true);
             int ins = 0, cc = -1;
             if (shape_hit(S, sid, type, flags, cas(S.geom) + off, ray, org, shift, t_dist, ins, cc, h.edge)) {
@@ -1343,7 +1376,7 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
       i = i + 1;
     } else {
       if (GENERAL && act && !hb) resume = nd.skip;
-      i = __ballot(hb) ? i + 1 : nd.skip;
+      i = hbm ? i + 1 : nd.skip;
     }
   }
   return any;
@@ -1361,6 +1394,7 @@ __device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams
 {
   float t_dist = FLT_MAX;
   bool any = false;
+  const unsigned long long am = __ballot(active);
   h.t_min = FLT_MAX;
   h.shape = -1;
   h.rank = 0x7fffffff;
@@ -1373,13 +1407,13 @@ __device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams
     if (!__ballot(active && !(h.t_min < tn))) break;
     const DNodeDev nd = cas(BUMP ? S.bnodes : S.fnodes)[node];
     const float tcull = h.t_min == FLT_MAX ? FLT_MAX : h.t_min * 1.0001f + 1e-4f;
-    bool hb = active & node_hit<false>(w, nd, 0.0f, org, tcull);
+    unsigned long long hbm = am & box_mask_finite(nd, w.rb, org, tcull);
     DT_WK(DT_WK_BOX, active);
-    DT_WK(DT_WK_BOX, BUMP && hb);
-    if (BUMP && __ballot(hb)) hb = hb & bump_leaf_gathered(S, w, nd.skip, shift, org);
+    DT_WK(DT_WK_BOX, BUMP && inv(hbm));
+    if (BUMP && hbm) hbm = __ballot(inv(hbm) & bump_leaf_gathered(S, w, nd.skip, shift, org));
     DT_WORK(cnt.wnodes++);
     DT_CNT(26);
-    if (__ballot(hb)) {
+    if (hbm) {
       const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
       const int rank = (int)(nd.meta >> 16);
       for (int q = 0; q < nq; ++q) {
@@ -1388,7 +1422,7 @@ __device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams
         leaf_shape(S, nd, q, sid, type, flags, off2);
         DT_CNT(8);
         DT_CNT(10 + (type & 7));
-        if (hb) {
+        if (inv(hbm)) {
           DT_WK(DT_WK_HIT_SHAPE + type, true);
           int ins = 0, cc = -1;
           if (shape_hit(S, sid, type, flags, cas(S.geom) + off2, ray, org, BUMP ? shift : 0.0f, t_dist, ins, cc, h.edge)) {
@@ -1434,10 +1468,12 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
   return any;
 }
 
-// intersectShadow over a gathered leaf's shapes for the lanes with `hb` (cpp:832-852)
+// intersectShadow over a gathered leaf's shapes (cpp:832-852) for the lanes of hbm that are not
+// occluded yet; om collects the occluded lanes
 template <class CNT>
-__device__ __forceinline__ void shadow_leaf(const DScene& S, const DNodeDev& nd, bool hb, bool& occl, V3 sn, V3 sstart,
-                                            float t_max, int skip_shape, float shift, CNT& cnt)
+__device__ __forceinline__ void shadow_leaf(const DScene& S, const DNodeDev& nd, unsigned long long hbm,
+                                            unsigned long long& om, V3 sn, V3 sstart, float t_max, int skip_shape,
+                                            float shift, CNT& cnt)
 {
   DT_T(q0);
   const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
@@ -1450,27 +1486,26 @@ __device__ __forceinline__ void shadow_leaf(const DScene& S, const DNodeDev& nd,
 #ifdef DT_STAMPS
     cnt.ph[42 + cnt.cur_path] += 1;   // wave-level shadow prim tests by path
 #endif
-    const bool test = hb && !occl && sid != skip_shape;
-#ifdef DT_STAMPS
-    const unsigned long long occ_before = __ballot(occl);
-#endif
-    if (test) {
+    const unsigned long long tm = sid != skip_shape ? hbm & ~om : 0ull;   // lanes that test this shape
+    bool o = false;
+    if (inv(tm)) {
       DT_WK(DT_WK_SHADOW_SHAPE + type, true);
-      if (shape_shadow(type, flags, cas(S.geom) + off, sn, sstart, t_max, shift)) occl = true;
+      o = shape_shadow(type, flags, cas(S.geom) + off, sn, sstart, t_max, shift);
     }
+    const unsigned long long om_new = __ballot(o);
 #ifdef DT_STAMPS
-    cnt.ph[47 + (type & 7)] += __popcll(__ballot(test));
-    cnt.ph[55 + (type & 7)] += __popcll(__ballot(occl) & ~occ_before);
-    {   // per (light, shape): waves, lanes, hits (ballots taken by the whole wave, added by lane 0)
-      const unsigned long long bt = __ballot(test), bo = __ballot(occl) & ~occ_before;
+    cnt.ph[47 + (type & 7)] += __popcll(tm);
+    cnt.ph[55 + (type & 7)] += __popcll(om_new);
+    {   // per (light, shape): waves, lanes, hits (added by lane 0)
       if ((threadIdx.x & 63) == 0 && sid < 254 && cnt.cur_li < 8) {
         unsigned long long* h = S.stats + ST_N + 1 + 64 + 3 * (cnt.cur_li * 256 + sid);
         atomicAdd(h, 1ull);
-        atomicAdd(h + 1, (unsigned long long)__popcll(bt));
-        atomicAdd(h + 2, (unsigned long long)__popcll(bo));
+        atomicAdd(h + 1, (unsigned long long)__popcll(tm));
+        atomicAdd(h + 2, (unsigned long long)__popcll(om_new));
       }
     }
 #endif
+    om |= om_new;
   }
   DT_T(q1);
   DT_ACC(32, q0, q1);
@@ -1494,7 +1529,8 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
   const bool ftree = !BUMP && !GENERAL && P.n_fnodes > 0 && (P.ftree_mode & 2);
   const DNodeDev* const NODES = BUMP ? S.bnodes : ftree ? S.fnodes : S.nodes;   // any-hit: order free
   int resume = active ? 0 : 0x7fffffff;
-  bool occl = false;
+  const unsigned long long am = __ballot(active);
+  unsigned long long om = 0;   // occluded lanes
   const float tcull = (DT_WITH_RPC && P.no_cull) ? FLT_MAX : shadow_tcull(t_max);
   int i = 0;
 #ifdef DT_STAMPS
@@ -1503,8 +1539,9 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
   const int n_nodes = BUMP ? P.n_bnodes : ftree ? P.n_fnodes : P.n_nodes;
   while (i < n_nodes) {
     const DNodeDev nd = cas(NODES)[i];
-    const bool act = GENERAL ? resume <= i : active & !occl;   // see closest_hit_walk
-    bool hb = act & node_hit<GENERAL>(w, nd, shift, bstart, tcull);
+    const bool act = GENERAL ? resume <= i : inv(am & ~om);   // see closest_hit_walk
+    unsigned long long hbm = node_mask<GENERAL>(w, nd, shift, bstart, tcull, am & ~om, act);
+    const bool hb = inv(hbm);
     DT_WORK(cnt.wnodes++);
     DT_WK(DT_WK_BOX, act);
     DT_CNT(27);
@@ -1513,28 +1550,27 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
 #endif
     if (nd.meta & DN_LEAF) {
       DT_WK(DT_WK_BOX, BUMP && hb);
-      if (BUMP && __ballot(hb)) hb = hb & bump_leaf_gathered(S, w, nd.skip, shift, bstart);
-      if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, shift, cnt);
+      if (BUMP && hbm) hbm = __ballot(hb & bump_leaf_gathered(S, w, nd.skip, shift, bstart));
+      if (hbm) shadow_leaf(S, nd, hbm, om, sn, sstart, t_max, skip_shape, shift, cnt);
       if (GENERAL) {
-        if (act) resume = occl ? 0x7fffffff : nd.skip;
+        if (act) resume = inv(om) ? 0x7fffffff : nd.skip;
         if (!__ballot(resume != 0x7fffffff)) break;
-      } else if (!__ballot(active & !occl)) {
+      } else if (!(am & ~om)) {
         break;
       }
       i = i + 1;
     } else {
       if (GENERAL && act && !hb) resume = nd.skip;
-      i = __ballot(hb) ? i + 1 : nd.skip;
+      i = hbm ? i + 1 : nd.skip;
     }
   }
 #ifdef DT_STAMPS
   {   // walks whose active lanes all ended occluded (28 visits, 29 walks) / none occluded (30, 31)
-    const unsigned long long va = __ballot(active), vo = __ballot(occl);
-    if (va && vo == va) { cnt.ph[28] += nv; cnt.ph[29] += 1; }
-    if (va && vo == 0) { cnt.ph[30] += nv; cnt.ph[31] += 1; }
+    if (am && om == am) { cnt.ph[28] += nv; cnt.ph[29] += 1; }
+    if (am && om == 0) { cnt.ph[30] += nv; cnt.ph[31] += 1; }
   }
 #endif
-  return occl;
+  return inv(om);
 }
 
 // The shadow test over a cell's candidate list (host_shadowgrid.cpp): the same box test and
@@ -1544,20 +1580,22 @@ template <bool BUMP, class CNT>
 __device__ bool occluded_list(const DScene& S, const Walk& w, bool active, V3 bstart, V3 sn, V3 sstart, float t_max,
                               int skip_shape, float shift, uint32_t off, uint32_t n, CNT& cnt)
 {
-  bool occl = false;
+  const unsigned long long am = __ballot(active);
+  unsigned long long om = 0;
   const float tcull = shadow_tcull(t_max);
   for (uint32_t k = 0; k < n; ++k) {
     const int r = uni(cas(S.sg_list)[off + k]);
     const DNodeDev nd = cas(S.nodes)[r];
-    const bool hb = active & !occl &
-                    (BUMP ? bump_leaf_gathered(S, w, r, shift, bstart) : node_hit<false>(w, nd, 0.0f, bstart, tcull));
-    DT_WK(DT_WK_BOX, active & !occl);
-    DT_WK(DT_WK_BOX, BUMP && active && !occl);
+    const bool live = inv(am & ~om);
+    const unsigned long long hbm = BUMP ? __ballot(live & bump_leaf_gathered(S, w, r, shift, bstart))
+                                        : (am & ~om) & box_mask_finite(nd, w.rb, bstart, tcull);
+    DT_WK(DT_WK_BOX, live);
+    DT_WK(DT_WK_BOX, BUMP && live);
     DT_CNT(34);
-    if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, shift, cnt);
-    if (!__ballot(active & !occl)) break;
+    if (hbm) shadow_leaf(S, nd, hbm, om, sn, sstart, t_max, skip_shape, shift, cnt);
+    if (!(am & ~om)) break;
   }
-  return occl;
+  return inv(om);
 }
 
 // wave minimum of a per-lane int, returned wave-uniform: DPP within rows of 16 (quad perms, half
@@ -1586,29 +1624,31 @@ template <bool BUMP, class CNT>
 __device__ bool occluded_union(const DScene& S, const Walk& w, bool active, V3 bstart, V3 sn, V3 sstart, float t_max,
                                int skip_shape, float shift, uint32_t off, uint32_t n, CNT& cnt)
 {
-  bool occl = false;
+  const unsigned long long am = __ballot(active);
+  unsigned long long om = 0;
   const float tcull = shadow_tcull(t_max);
   uint32_t k = 0;
   // head: the lane's next leaf; nxt: the one after it, loaded an iteration ahead
   int head = (active && n > 0) ? S.sg_list[off] : INT_MAX;
   int nxt = (active && n > 1) ? S.sg_list[off + 1] : INT_MAX;
   while (true) {
-    const int m = wave_min_u(occl ? INT_MAX : head);
+    const int m = wave_min_u(inv(om) ? INT_MAX : head);
     if (m == INT_MAX) break;
     const DNodeDev nd = cas(S.nodes)[m];
-    const bool hb = active & !occl &
-                    (BUMP ? bump_leaf_gathered(S, w, m, shift, bstart) : node_hit<false>(w, nd, 0.0f, bstart, tcull));
-    DT_WK(DT_WK_BOX, active & !occl);
-    DT_WK(DT_WK_BOX, BUMP && active && !occl);
+    const bool live = inv(am & ~om);
+    const unsigned long long hbm = BUMP ? __ballot(live & bump_leaf_gathered(S, w, m, shift, bstart))
+                                        : (am & ~om) & box_mask_finite(nd, w.rb, bstart, tcull);
+    DT_WK(DT_WK_BOX, live);
+    DT_WK(DT_WK_BOX, BUMP && live);
     DT_CNT(34);
-    if (__ballot(hb)) shadow_leaf(S, nd, hb, occl, sn, sstart, t_max, skip_shape, shift, cnt);
+    if (hbm) shadow_leaf(S, nd, hbm, om, sn, sstart, t_max, skip_shape, shift, cnt);
     if (head == m) {
       ++k;
       head = nxt;
       nxt = k + 1 < n ? S.sg_list[off + k + 1] : INT_MAX;
     }
   }
-  return occl;
+  return inv(om);
 }
 
 // shading point in grid-cell coordinates
@@ -2718,14 +2758,16 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   dn.pair = dn_pair;
 #endif
 
-  int64_t item = 0, batch_end = 0;
+  // items are dequeued P.item_batch at a time (one same-address atomic per batch). The first batch
+  // of every wave is its own by block index: 5120 waves starting at once would otherwise queue
+  // behind one another on the one atomic word; the shared counter hands out the items after them.
+  const int batch = P.item_batch > 1 ? P.item_batch : 1;
+  int64_t item = (int64_t)blockIdx.x * batch, batch_end = item + batch;
   while (true) {
-    // items are dequeued P.item_batch at a time (one same-address atomic per batch)
     if (item >= batch_end) {
-      const int batch = P.item_batch > 1 ? P.item_batch : 1;
       if (lane == 0) item_s = atomicAdd(S.queue, (unsigned long long)batch);
       __syncthreads();
-      item = (int64_t)item_s;
+      item = (int64_t)item_s + (int64_t)gridDim.x * batch;
       batch_end = item + batch;
       __syncthreads();
     }
