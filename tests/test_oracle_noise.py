@@ -41,6 +41,33 @@ def test_cloud_march_points_bit_exact():
     assert np.array_equal(got, d["march_value"])
 
 
+def test_cloud_band_bound():
+    """The bound behind the sky kernels' band test (dt_kernels.hip, DT_CLOUD_ABOVE/BELOW):
+    |ValueNoise_3D| <= 1.875, so a march step with p.y + cloudhoff >= 1.3126 adds nothing and one
+    with p.y + cloudhoff <= -2.3126 has density exactly 1 (cpp:175-179), whatever the noise."""
+    o = oracle.oracle()
+    # Noise3D in [1 - (2^31-1)/denom, 1]; Smoothed3D's weights sum to 1 (noise.h:52-55)
+    lo = 1.0 - 0x7fffffff / 1073741823
+    assert -1.0000000019 < lo < -1.0
+    assert abs(9.0 / 18 + 8 * 2.0 / 144 + 6 * 4.0 / 108 + 12 * 3.0 / 216 - 1.0) < 1e-15
+    rng = np.random.default_rng(3)
+    pts = rng.uniform(-60, 60, (4000, 3))
+    vn = np.array([o.or_value_noise3d(*map(float, p)) for p in pts])
+    assert np.abs(vn).max() <= 1.875
+    nmax = float(np.float32(0.7 * 1.8750000036))
+    assert nmax <= 1.3125002
+    h = float(np.float32(0.2))
+    for y in np.concatenate([np.linspace(-40, 40, 4001), 1.3126 - h + np.linspace(0, 1e-6, 11),
+                             -2.3126 - h - np.linspace(0, 1e-6, 11)]):
+        yh = float(y) + h
+        for noise in (-nmax, nmax, 0.0):
+            cd = np.float32((float(y) + noise) + h)
+            if yh >= 1.3126:
+                assert cd >= 0
+            if yh <= -2.3126:
+                assert min(1.0, abs(float(cd))) == 1.0
+
+
 def test_against_reference_build_if_present():
     r = oracle.ref_noise()
     if r is None:

@@ -20,6 +20,7 @@ CASES = [  # (name, builder, frame, models, W, H, spp, depth, world)
     ("c4_1of256", "final", 240, 1, 1920, 1080, 256, 8, 256),
     ("c5_1088_1of512", "final", 1088, 0, 3840, 2160, 64, 10, 512),
     ("c5_1920_1of512", "final", 1920, 0, 3840, 2160, 64, 10, 512),
+    ("c5_2200_cloud_1of64", "final", 2200, 0, 3840, 2160, 1, 10, 64),
 ]
 
 
