@@ -32,6 +32,10 @@ extern "C" hipError_t dt_launch_normalize(const double* in, double* out, int64_t
 extern "C" const void* dt_trace_kernel_dn_ptr(void);
 extern "C" hipError_t dt_launch_trace_w5(const void* dev_launch, float* out, int grid, hipStream_t stream);
 extern "C" const void* dt_trace_kernel_w5_ptr(void);
+extern "C" hipError_t dt_launch_trace_blur(const void* dev_launch, float* out, int grid, hipStream_t stream);
+extern "C" const void* dt_trace_kernel_blur_ptr(void);
+extern "C" hipError_t dt_launch_trace_w5_blur(const void* dev_launch, float* out, int grid, hipStream_t stream);
+extern "C" const void* dt_trace_kernel_w5_blur_ptr(void);
 extern "C" hipError_t dt_launch_isect(const void* dev_launch, int64_t first, int64_t n, int32_t* hit_shape, float* hit_t,
                                       int grid, hipStream_t stream);
 extern "C" const void* dt_isect_kernel_ptr(void);
@@ -673,12 +677,22 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   // DT_W5=0 never, DT_W5=1 at any spp with at most 8 pixels per wave (its per-pixel sums have 8 slots).
   const char* w5_env = getenv("DT_W5");
   const bool w5 = !sc->no_cull && !donate && P.ppw <= 8 && (w5_env ? w5_env[0] == '1' : P.spp >= 64);
-  static int resident = 0, resident_rpc = 0, resident_dn = 0, resident_w5 = 0;
-  if (!resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
+  // below frame_prism every motion-blur pass shifts by 0 (the reference's val, Q19), so those frames
+  // take the product kernels built without the shift paths (dt_kernels.hip DT_NOSHIFT); later
+  // frames the *_blur builds of the same kernels (DT_BLUR_KERNEL=1: those for every frame, the tests'
+  // check of the two builds against each other)
+  const char* bk_env = getenv("DT_BLUR_KERNEL");
+  const bool blur = P.frame >= P.frame_prism || (bk_env && bk_env[0] == '1');
+  static int resident = 0, resident_rpc = 0, resident_dn = 0, resident_w5 = 0, resident_b = 0, resident_w5b = 0;
+  const bool w4 = !sc->no_cull && !donate && !w5;
+  if (w4 && !blur && !resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
+  if (w4 && blur && !resident_b) resident_b = max_resident_waves(dt_trace_kernel_blur_ptr(), 64);
   if (sc->no_cull && !resident_rpc) resident_rpc = max_resident_waves(dt_trace_kernel_rpc_ptr(), 64);
   if (donate && !resident_dn) resident_dn = max_resident_waves(dt_trace_kernel_dn_ptr(), 64);
-  if (w5 && !resident_w5) resident_w5 = max_resident_waves(dt_trace_kernel_w5_ptr(), 64);
-  const int64_t waves = sc->no_cull ? resident_rpc : donate ? resident_dn : w5 ? resident_w5 : resident;
+  if (w5 && !blur && !resident_w5) resident_w5 = max_resident_waves(dt_trace_kernel_w5_ptr(), 64);
+  if (w5 && blur && !resident_w5b) resident_w5b = max_resident_waves(dt_trace_kernel_w5_blur_ptr(), 64);
+  const int64_t waves = sc->no_cull ? resident_rpc : donate ? resident_dn
+                        : w5 ? (blur ? resident_w5b : resident_w5) : (blur ? resident_b : resident);
   int64_t grid = P.n_items < waves ? P.n_items : waves;
   if (grid < 1) grid = 1;
   hs.dn_pool = nullptr;
@@ -738,10 +752,12 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   sc->copy_pending = true;
   HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 1 + DT_N_STAMPS), st));
   HIPCHK(hipEventRecord(sc->ev0, st));
-  HIPCHK(sc->no_cull ? dt_launch_trace_rpc(sc->d_launch, out_dev, (int)grid, st)
-         : donate   ? dt_launch_trace_dn(sc->d_launch, out_dev, (int)grid, st)
-         : w5       ? dt_launch_trace_w5(sc->d_launch, out_dev, (int)grid, st)
-                    : dt_launch_trace(sc->d_launch, out_dev, (int)grid, st));
+  HIPCHK(sc->no_cull      ? dt_launch_trace_rpc(sc->d_launch, out_dev, (int)grid, st)
+         : donate        ? dt_launch_trace_dn(sc->d_launch, out_dev, (int)grid, st)
+         : w5 && blur    ? dt_launch_trace_w5_blur(sc->d_launch, out_dev, (int)grid, st)
+         : w5            ? dt_launch_trace_w5(sc->d_launch, out_dev, (int)grid, st)
+         : blur          ? dt_launch_trace_blur(sc->d_launch, out_dev, (int)grid, st)
+                         : dt_launch_trace(sc->d_launch, out_dev, (int)grid, st));
   if (PL.sky_defer) HIPCHK(dt_launch_sky_miss(sc->d_launch, out_dev, n_px, st));
   HIPCHK(hipEventRecord(sc->ev1, st));
   sc->timed = true;

@@ -85,15 +85,29 @@ using namespace dtd;
 #ifndef DT_W5
 #define DT_W5 0
 #endif
+// DT_NOSHIFT=1 (build/dt_kernels.o, build/dt_kernels_w5.o): the product kernels for frames without
+// motion-blur shifts (frame < frame_prism, where the reference's blur value is 0, Q19: C1-C4 and
+// C5's room frames). shift is the constant 0, so the bump walks, bump lists and shifted shape tests
+// compile away. DT_NOSHIFT=0 (build/dt_kernels_blur.o, build/dt_kernels_w5_blur.o): the same kernels
+// with every shift path, named *_blur, for frames >= frame_prism (dt_api.cpp picks per launch).
+#ifndef DT_NOSHIFT
+#define DT_NOSHIFT 0
+#endif
 #if DT_WITH_RPC
 #define DT_TRACE_KERNEL dt_trace_kernel_rpc
-#elif DT_W5
+#elif DT_W5 && DT_NOSHIFT
 #define DT_TRACE_KERNEL dt_trace_kernel_w5
+#elif DT_W5
+#define DT_TRACE_KERNEL dt_trace_kernel_w5_blur
 #elif DT_DONATE
 #define DT_TRACE_KERNEL dt_trace_kernel_dn
-#else
+#elif DT_NOSHIFT
 #define DT_TRACE_KERNEL dt_trace_kernel
+#else
+#define DT_TRACE_KERNEL dt_trace_kernel_blur
 #endif
+// the 4-wave still build also carries the small kernels and the launch-record helpers
+#define DT_HELPERS (!DT_WITH_RPC && !DT_DONATE && !DT_ISECT && !DT_W5 && DT_NOSHIFT)
 
 #define DT_STACK_MAX 48
 #define DT_MAX_CLOUD_STEPS 2048
@@ -341,13 +355,28 @@ __device__ V3 cloud_finish(const DParams& P, V3 color)
   return sub(mul(1 + P.saturation, color), mul(P.saturation, grey));
 }
 
+// The cloud band of one march step (cpp:175-179), decided without the noise where its bound
+// settles it. |ValueNoise_3D| <= 1.875 (4 octaves of amplitudes 1/8..1; each Smoothed3D is a
+// convex combination of Noise3D values in [-1.0000000019, 1], each cosInterpolate a convex
+// combination), so |noise| = |float(0.7 * vn)| <= 1.3125002. With yh = p.y + cloudhoff:
+//   yh >= 1.3126:  clouddistance >= 9.9e-5 > 0, the step adds nothing;
+//   yh <= -2.3126: clouddistance <= -1.00009, so density = clamp(|cd|) = 1 exactly.
+// The margins dwarf the roundings of the two double additions and the float conversion
+// (about |p.y| * 2^-52, below 1e-9 for any |p.y| < 1e6; a NaN yh fails both tests and marches).
+// Only steps in between evaluate the noise.
+#define DT_CLOUD_ABOVE 1.3126
+#define DT_CLOUD_BELOW (-2.3126)
+
 // full cloudColor on one lane
 __device__ __forceinline__ V3 cloud_color_lane(const DParams& P, const float* __restrict__ zs, V3 ray)
 {
   V3 sky = sky_color(P, ray);
   V3 color = sky;
   for (int s = 0; s < P.n_cloud_steps; ++s) {
-    float d = cloud_step(P, zs[s], ray);
+    const float z = zs[s];
+    const double yh = (double)z * ray.y + (double)P.cloudhoff;
+    if (yh >= DT_CLOUD_ABOVE) continue;
+    float d = yh <= DT_CLOUD_BELOW ? 1.0f : cloud_step(P, z, ray);
     if (d >= 0.0f) {
       color.x = cloud_apply(color.x, sky.z, d);
       color.y = cloud_apply(color.y, sky.y, d);
@@ -450,10 +479,11 @@ __device__ __forceinline__ V3 G3(GP g, int o) { return v3(g[o], g[o + 1], g[o + 
 
 // Rectangle plane + quad bounds test (geometry.cpp:640-741 / 2292-2312): R record
 // tlim: the caller discards t >= tlim (shadow tests: t_max), so such planes may be rejected early
-__device__ __forceinline__ bool rect_hit_R(GP R, V3 ray, V3 start, float eps,
-                                           float& t_out, float& ch1, float& ch2, float tlim = INFINITY)
+// A: the corner, R_A of the record unless a motion-blur pass moved it (shifted_exact)
+__device__ __forceinline__ bool rect_hit_RA(GP R, V3 A, V3 ray, V3 start, float eps,
+                                            float& t_out, float& ch1, float& ch2, float tlim = INFINITY)
 {
-  V3 A = G3(R, R_A), n = G3(R, R_N);
+  V3 n = G3(R, R_N);
   float dn = (float)dot(ray, n);
   if (dn == 0) return false;
   const double num = dot(sub(A, start), n);
@@ -481,6 +511,11 @@ __device__ __forceinline__ bool rect_hit_R(GP R, V3 ray, V3 start, float eps,
   }
   return false;
 }
+__device__ __forceinline__ bool rect_hit_R(GP R, V3 ray, V3 start, float eps,
+                                           float& t_out, float& ch1, float& ch2, float tlim = INFINITY)
+{
+  return rect_hit_RA(R, G3(R, R_A), ray, start, eps, t_out, ch1, ch2, tlim);
+}
 
 // same, R computed from (shifted) raw vertices — motion-blur retraces of "rectangle" shapes
 __device__ bool rect_hit_raw(V3 A, V3 B, V3 C, V3 D, V3 ray, V3 start, float eps, float& t_out)
@@ -507,6 +542,21 @@ __device__ __forceinline__ void shifted_rect(GP g, float shift, V3& A, V3& B,
 {
   A = G3(g, RC_A); B = G3(g, RC_B); C = G3(g, RC_C); D = G3(g, RC_D);
   A.y = A.y + shift; B.y = B.y + shift; C.y = C.y + shift; D.y = D.y + shift;
+}
+
+// A "rectangle" shifted by a motion-blur pass (cpp:1113; vertices' y + shift): when the shifted y
+// differences equal the unshifted ones, (P.y + s) - (A.y + s) == P.y - A.y for P = B, C, D, every
+// edge vector of the shifted rectangle is bit for bit the unshifted one, so the normal, edge
+// directions and lengths the reference recomputes per call (Rectangle::intersect, geometry.cpp:
+// 640-741) are the record's (the same IEEE expressions of the same operands); only the corner A
+// moves. Exact in the tunnel scenes for every shift tested (the y + s sums need no rounding); a
+// lane for which it fails takes rect_hit_raw.
+__device__ __forceinline__ bool shifted_exact(GP g, float shift, V3& As)
+{
+  const double ay = g[RC_A + 1], ays = ay + shift;
+  As = v3(g[RC_A], ays, g[RC_A + 2]);
+  return ((g[RC_B + 1] + shift) - ays == g[RC_B + 1] - ay) & ((g[RC_C + 1] + shift) - ays == g[RC_C + 1] - ay) &
+         ((g[RC_D + 1] + shift) - ays == g[RC_D + 1] - ay);
 }
 
 // quadratic of Sphere/Cylinder (geometry.cpp:108-124 / 246-256)
@@ -790,6 +840,11 @@ __device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, GP
       inside = 0;
       float tt, c1, c2;
       if ((flags & DT_F_NAMED_RECT) && shift != 0.0f) {
+        V3 As;
+        if (shifted_exact(g, shift, As)) {
+          if (rect_hit_RA(g + RC_R, As, ray, start, 1e-4f, tt, c1, c2)) { t = tt; return true; }
+          return false;
+        }
         V3 A, B, C, D;
         shifted_rect(g, shift, A, B, C, D);
         if (rect_hit_raw(A, B, C, D, ray, start, 1e-4f, tt)) { t = tt; return true; }
@@ -873,6 +928,8 @@ __device__ bool shape_shadow(int type, uint32_t flags, GP g, V3 ray, V3 start,
     }
     case DT_SHAPE_RECTANGLE:
       if ((flags & DT_F_NAMED_RECT) && shift != 0.0f) {
+        V3 As;
+        if (shifted_exact(g, shift, As)) return rect_hit_RA(g + RC_R, As, ray, start, 1e-4f, tt, a, b, t_max) && tt < t_max;
         V3 A, B, C, D;
         shifted_rect(g, shift, A, B, C, D);
         return rect_hit_raw(A, B, C, D, ray, start, 1e-4f, tt) && tt < t_max;
@@ -1202,7 +1259,7 @@ __device__ __forceinline__ Walk make_walk(const DParams& P, bool active, V3 ray,
   const bool odd = w.rb.ix | w.rb.iy | w.rb.iz | isnan(ray.x) | isnan(ray.y) | isnan(ray.z) | isnan(st.x) |
                    isnan(st.y) | isnan(st.z);
   w.inf_wave = __ballot(active && odd) != 0 || !P.boxes_ordered;
-  w.bump_wave = __ballot(active && shift != 0.0f) != 0;
+  w.bump_wave = !DT_NOSHIFT && __ballot(active && shift != 0.0f) != 0;
   return w;
 }
 
@@ -2046,7 +2103,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
   };
 #else
   const Ctx& c = c_in;
-  const float shift = shift_in;
+  const float shift = DT_NOSHIFT ? 0.0f : shift_in;
 #endif
   const DScene& S = *c.S;
   const DParams& P = *c.P;
@@ -2954,7 +3011,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
 
 #endif   // !DT_ISECT
 
-#if !DT_WITH_RPC && !DT_DONATE && !DT_ISECT && !DT_W5
+#if DT_HELPERS
 // The sky of the pixels a 1-spp trace launch flagged as missed (P.sky_defer): renderImage's miss
 // branch (cpp:1074-1092: cloudColor of mcam * focalPoint) one pixel per lane, at the occupancy of a
 // small kernel instead of inside the trace kernel's register budget. With one sample the pixel is
@@ -3097,7 +3154,7 @@ extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_
 }
 extern "C" const void* dt_trace_kernel_ptr(void) { return (const void*)dt_trace_kernel; }
 #elif DT_ISECT
-#elif DT_W5   // the trace kernel at 5 waves per SIMD
+#elif DT_W5 && DT_NOSHIFT   // the trace kernel at 5 waves per SIMD
 static_assert(DT_TRACE_MIN_WAVES == 5 && DT_PSUM_LDS == 2, "dt_kernels_w5.o: Makefile flags");
 extern "C" hipError_t dt_launch_trace_w5(const void* dev_launch, float* out, int grid, hipStream_t stream)
 {
@@ -3105,6 +3162,14 @@ extern "C" hipError_t dt_launch_trace_w5(const void* dev_launch, float* out, int
   return hipGetLastError();
 }
 extern "C" const void* dt_trace_kernel_w5_ptr(void) { return (const void*)dt_trace_kernel_w5; }
+#elif DT_W5   // the same with motion-blur shifts
+static_assert(DT_TRACE_MIN_WAVES == 5 && DT_PSUM_LDS == 2, "dt_kernels_w5_blur.o: Makefile flags");
+extern "C" hipError_t dt_launch_trace_w5_blur(const void* dev_launch, float* out, int grid, hipStream_t stream)
+{
+  hipLaunchKernelGGL(dt_trace_kernel_w5_blur, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
+  return hipGetLastError();
+}
+extern "C" const void* dt_trace_kernel_w5_blur_ptr(void) { return (const void*)dt_trace_kernel_w5_blur; }
 #elif DT_DONATE   // the trace kernel with DFS work sharing inside the wave
 extern "C" hipError_t dt_launch_trace_dn(const void* dev_launch, float* out, int grid, hipStream_t stream)
 {
@@ -3112,6 +3177,13 @@ extern "C" hipError_t dt_launch_trace_dn(const void* dev_launch, float* out, int
   return hipGetLastError();
 }
 extern "C" const void* dt_trace_kernel_dn_ptr(void) { return (const void*)dt_trace_kernel_dn; }
+#elif !DT_WITH_RPC   // the 4-wave trace kernel with motion-blur shifts
+extern "C" hipError_t dt_launch_trace_blur(const void* dev_launch, float* out, int grid, hipStream_t stream)
+{
+  hipLaunchKernelGGL(dt_trace_kernel_blur, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
+  return hipGetLastError();
+}
+extern "C" const void* dt_trace_kernel_blur_ptr(void) { return (const void*)dt_trace_kernel_blur; }
 #else   // DT_WITH_RPC: the trace kernel for scenes with a RectPrismWithCylinder
 extern "C" hipError_t dt_launch_trace_rpc(const void* dev_launch, float* out, int grid, hipStream_t stream)
 {

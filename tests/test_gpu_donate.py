@@ -6,6 +6,8 @@ product kernel's (and the oracle's) with the same rays traced. The cases are the
 a C3 share of the 8-way tile split (the deep glossy column), C5's room-to-tunnel transition frame
 (8 rays per sample), a motion-blur frame (in_motion, Q6, is the last rayColor's: kept as the
 value of the largest pre-order path, whoever ran that node) and C2's full frame.
+
+Also the other per-launch kernel choice: still frames' kernels against their motion-blur builds.
 """
 import numpy as np
 import pytest
@@ -72,3 +74,26 @@ def test_set_kernel_rejects_unknown_choice(cuda):
         scene.set_kernel(k)
     assert dt.lib.dt_scene_set_kernel(scene.handle, 7) == -1
     scene.close()
+
+
+BLUR_CASES = [  # (id, builder args, frame, tile world): still frames, 5-wave (64 spp) and 4-wave (16 spp)
+    ("c3_1of64_w5", ("final", 240, 0, 1920, 1080, 64, 8), 240, 64),
+    ("c2_full_w4", ("final", 240, 0, 800, 600, 16, 4), 240, 1),
+    ("c5_room_480_1of512_w5", ("final", 480, 0, 3840, 2160, 64, 10), 480, 512),
+]
+
+
+@pytest.mark.parametrize("case", BLUR_CASES, ids=[c[0] for c in BLUR_CASES])
+def test_still_kernels_match_blur_builds(cuda, monkeypatch, case):
+    """Frames below frame_prism take the product kernels built without the motion-blur shift paths
+    (dt_kernels.hip DT_NOSHIFT); DT_BLUR_KERNEL=1 renders them with the *_blur builds, which every
+    later frame takes. Same rays, same bits."""
+    label, args, frame, world = case
+    g, built = _globals(*args)
+    tile = dt.tiles(rank=0, world=world, layout=dt.DT_OUT_SLAB) if world > 1 else dt.tiles()
+    monkeypatch.setenv("DT_BLUR_KERNEL", "0")
+    still, st0 = _render(g, built, frame, tile, False, monkeypatch)
+    monkeypatch.setenv("DT_BLUR_KERNEL", "1")
+    blur, st1 = _render(g, built, frame, tile, False, monkeypatch)
+    assert st0.rays == st1.rays and st0.shadow_rays == st1.shadow_rays
+    log_equal("%s still kernel vs blur build (bits)" % label, still.view(np.uint32), blur.view(np.uint32))
