@@ -198,12 +198,14 @@ def valu_roofline(cfg, kernel_ms, samples, ref_work=None, ref_samples=0, pmc=Non
     return r
 
 
-def trace_kernel_name(spp):
-    """the trace kernel dt_render launches for this spp (dt_api.cpp enqueue_render: the 5-wave build
-    at one pixel per wave, spp >= 64, unless DT_W5 says otherwise)"""
+def trace_kernel_name(spp, models):
+    """the trace kernel dt_render launches for the bench configs (frame 240, a still frame;
+    dt_api.cpp enqueue_render): the 5-wave build at one pixel per wave, spp >= 64, unless DT_W5 says
+    otherwise; the room build without OBJ models, the *_full build with their triangles (C4)"""
     e = os.environ.get("DT_W5")
     ppw = 64 // min(spp, 64)
-    return "dt_trace_kernel_w5" if ppw <= 8 and (e[:1] == "1" if e else spp >= 64) else "dt_trace_kernel"
+    name = "dt_trace_kernel_w5" if ppw <= 8 and (e[:1] == "1" if e else spp >= 64) else "dt_trace_kernel"
+    return name + "_full" if models else name
 
 
 def load_pmc_traffic():
@@ -351,11 +353,11 @@ def main():
         roof = None
         if world == 1 and not args.no_roofline:
             roof = valu_roofline(args.config, kernel_ms, W * H * spp, ref_work, ref_samples,
-                                 pmc if pmc.get("kernel") == trace_kernel_name(spp) else None)
+                                 pmc if pmc.get("kernel") == trace_kernel_name(spp, g.use_model) else None)
         if roof is not None:
-            roof["kernel"] = trace_kernel_name(spp)
+            roof["kernel"] = trace_kernel_name(spp, g.use_model)
         if roof is None:   # no diagnostic library (or N > 1): the HBM line alone
-            roof = dict(hbm, kernel=trace_kernel_name(spp), kernel_ms=round(kernel_ms, 3))
+            roof = dict(hbm, kernel=trace_kernel_name(spp, g.use_model), kernel_ms=round(kernel_ms, 3))
         else:
             roof["hbm"] = hbm
         if pmc.get("valu_active_per_wave_cycle"):

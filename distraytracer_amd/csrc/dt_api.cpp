@@ -19,23 +19,24 @@ using namespace dth;
 extern "C" size_t dt_launch_size(void);
 extern "C" size_t dt_scene_struct_offset(void);
 extern "C" size_t dt_params_struct_offset(void);
-extern "C" hipError_t dt_launch_trace(const void* dev_launch, float* out, int grid, hipStream_t stream);
 extern "C" hipError_t dt_launch_sky(const void* dev_launch, float* out, int64_t n_threads, hipStream_t stream);
 extern "C" hipError_t dt_launch_sky_miss(const void* dev_launch, float* out, int64_t n_px, hipStream_t stream);
 extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_t slab_floats, const float* slabs,
                                        float* image, hipStream_t stream);
-extern "C" const void* dt_trace_kernel_ptr(void);
-extern "C" hipError_t dt_launch_trace_rpc(const void* dev_launch, float* out, int grid, hipStream_t stream);
-extern "C" const void* dt_trace_kernel_rpc_ptr(void);
-extern "C" hipError_t dt_launch_trace_dn(const void* dev_launch, float* out, int grid, hipStream_t stream);
 extern "C" hipError_t dt_launch_normalize(const double* in, double* out, int64_t n, hipStream_t stream);
-extern "C" const void* dt_trace_kernel_dn_ptr(void);
-extern "C" hipError_t dt_launch_trace_w5(const void* dev_launch, float* out, int grid, hipStream_t stream);
-extern "C" const void* dt_trace_kernel_w5_ptr(void);
-extern "C" hipError_t dt_launch_trace_blur(const void* dev_launch, float* out, int grid, hipStream_t stream);
-extern "C" const void* dt_trace_kernel_blur_ptr(void);
-extern "C" hipError_t dt_launch_trace_w5_blur(const void* dev_launch, float* out, int grid, hipStream_t stream);
-extern "C" const void* dt_trace_kernel_w5_blur_ptr(void);
+// the trace-kernel builds (dt_kernels.hip DT_TRACE_KERNEL, Makefile TRACE_BUILDS)
+#define DT_TRACE_BUILD(k)                                                                              \
+  extern "C" hipError_t k##_launch(const void* dev_launch, float* out, int grid, hipStream_t stream); \
+  extern "C" const void* k##_ptr(void);
+DT_TRACE_BUILD(dt_trace_kernel)
+DT_TRACE_BUILD(dt_trace_kernel_full)
+DT_TRACE_BUILD(dt_trace_kernel_blur)
+DT_TRACE_BUILD(dt_trace_kernel_w5)
+DT_TRACE_BUILD(dt_trace_kernel_w5_full)
+DT_TRACE_BUILD(dt_trace_kernel_w5_blur)
+DT_TRACE_BUILD(dt_trace_kernel_dn)
+DT_TRACE_BUILD(dt_trace_kernel_rpc)
+#undef DT_TRACE_BUILD
 extern "C" hipError_t dt_launch_isect(const void* dev_launch, int64_t first, int64_t n, int32_t* hit_shape, float* hit_t,
                                       int grid, hipStream_t stream);
 extern "C" const void* dt_isect_kernel_ptr(void);
@@ -148,6 +149,7 @@ struct dt_scene {
   float bump_pad = 0;          // y padding of its leaves: the largest |shift| a blur pass can draw
   bool bump_up_only = false;   // bump tree / blur-padded lists built for shifts >= 0 only
   bool no_cull = false;        // a RectPrismWithCylinder: no t-culling, no grid, no primary lists
+  bool room = false;           // every feature within DT_ROOM_FEATURES: the room builds can render it
   int kernel = DT_KERNEL_AUTO; // dt_scene_set_kernel
   ShadowGrid sg;
   void* d_sg_cells = nullptr;
@@ -288,6 +290,19 @@ int dt_scene_prepare(const dt_scene_desc* desc, const dt_globals* g, dt_scene** 
   if (rc) {
     delete s;
     return fail(rc, err);
+  }
+  {   // the scene's features (dt_scene_dev.h): whether the room builds of the trace kernel cover it
+    unsigned feat = 0;
+    for (int i = 0; i < desc->n_shapes; ++i) {
+      const int t = desc->shapes[i].type;
+      feat |= (t >= 0 && t < DT_FEAT_SPHL) ? 1u << t : 1u << 31;
+      if (desc->shapes[i].model == DT_MODEL_OREN_NAYAR) feat |= 1u << DT_FEAT_ON;
+    }
+    for (int i = 0; i < desc->n_lights; ++i) {
+      const int t = desc->lights[i].type;
+      if (t != DT_LIGHT_POINT && t != DT_LIGHT_RECT) feat |= 1u << DT_FEAT_SPHL;
+    }
+    s->room = (feat & ~DT_ROOM_FEATURES) == 0;
   }
   if (hipGetDevice(&s->device) != hipSuccess) {
     delete s;
@@ -678,21 +693,23 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   const char* w5_env = getenv("DT_W5");
   const bool w5 = !sc->no_cull && !donate && P.ppw <= 8 && (w5_env ? w5_env[0] == '1' : P.spp >= 64);
   // below frame_prism every motion-blur pass shifts by 0 (the reference's val, Q19), so those frames
-  // take the product kernels built without the shift paths (dt_kernels.hip DT_NOSHIFT); later
-  // frames the *_blur builds of the same kernels (DT_BLUR_KERNEL=1: those for every frame, the tests'
-  // check of the two builds against each other)
+  // take the product kernels built without the shift paths (dt_kernels.hip DT_NOSHIFT), room scenes
+  // the builds without the shape types, lights and materials they lack (DT_FEATURES); later frames
+  // the *_blur builds (DT_BLUR_KERNEL=1: those for every frame, the tests' check of the builds
+  // against each other)
   const char* bk_env = getenv("DT_BLUR_KERNEL");
   const bool blur = P.frame >= P.frame_prism || (bk_env && bk_env[0] == '1');
-  static int resident = 0, resident_rpc = 0, resident_dn = 0, resident_w5 = 0, resident_b = 0, resident_w5b = 0;
-  const bool w4 = !sc->no_cull && !donate && !w5;
-  if (w4 && !blur && !resident) resident = max_resident_waves(dt_trace_kernel_ptr(), 64);
-  if (w4 && blur && !resident_b) resident_b = max_resident_waves(dt_trace_kernel_blur_ptr(), 64);
-  if (sc->no_cull && !resident_rpc) resident_rpc = max_resident_waves(dt_trace_kernel_rpc_ptr(), 64);
-  if (donate && !resident_dn) resident_dn = max_resident_waves(dt_trace_kernel_dn_ptr(), 64);
-  if (w5 && !blur && !resident_w5) resident_w5 = max_resident_waves(dt_trace_kernel_w5_ptr(), 64);
-  if (w5 && blur && !resident_w5b) resident_w5b = max_resident_waves(dt_trace_kernel_w5_blur_ptr(), 64);
-  const int64_t waves = sc->no_cull ? resident_rpc : donate ? resident_dn
-                        : w5 ? (blur ? resident_w5b : resident_w5) : (blur ? resident_b : resident);
+  struct Build { hipError_t (*launch)(const void*, float*, int, hipStream_t); const void* (*ptr)(void); int resident; };
+  static Build builds[8] = {
+      {dt_trace_kernel_launch, dt_trace_kernel_ptr, 0},           {dt_trace_kernel_full_launch, dt_trace_kernel_full_ptr, 0},
+      {dt_trace_kernel_blur_launch, dt_trace_kernel_blur_ptr, 0}, {dt_trace_kernel_w5_launch, dt_trace_kernel_w5_ptr, 0},
+      {dt_trace_kernel_w5_full_launch, dt_trace_kernel_w5_full_ptr, 0},
+      {dt_trace_kernel_w5_blur_launch, dt_trace_kernel_w5_blur_ptr, 0},
+      {dt_trace_kernel_dn_launch, dt_trace_kernel_dn_ptr, 0},     {dt_trace_kernel_rpc_launch, dt_trace_kernel_rpc_ptr, 0}};
+  const int variant = blur ? 2 : sc->room ? 0 : 1;
+  Build& kb = sc->no_cull ? builds[7] : donate ? builds[6] : builds[(w5 ? 3 : 0) + variant];
+  if (!kb.resident) kb.resident = max_resident_waves(kb.ptr(), 64);
+  const int64_t waves = kb.resident;
   int64_t grid = P.n_items < waves ? P.n_items : waves;
   if (grid < 1) grid = 1;
   hs.dn_pool = nullptr;
@@ -752,12 +769,7 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   sc->copy_pending = true;
   HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 1 + DT_N_STAMPS), st));
   HIPCHK(hipEventRecord(sc->ev0, st));
-  HIPCHK(sc->no_cull      ? dt_launch_trace_rpc(sc->d_launch, out_dev, (int)grid, st)
-         : donate        ? dt_launch_trace_dn(sc->d_launch, out_dev, (int)grid, st)
-         : w5 && blur    ? dt_launch_trace_w5_blur(sc->d_launch, out_dev, (int)grid, st)
-         : w5            ? dt_launch_trace_w5(sc->d_launch, out_dev, (int)grid, st)
-         : blur          ? dt_launch_trace_blur(sc->d_launch, out_dev, (int)grid, st)
-                         : dt_launch_trace(sc->d_launch, out_dev, (int)grid, st));
+  HIPCHK(kb.launch(sc->d_launch, out_dev, (int)grid, st));
   if (PL.sky_defer) HIPCHK(dt_launch_sky_miss(sc->d_launch, out_dev, n_px, st));
   HIPCHK(hipEventRecord(sc->ev1, st));
   sc->timed = true;

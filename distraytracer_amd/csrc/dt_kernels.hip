@@ -93,21 +93,37 @@ using namespace dtd;
 #ifndef DT_NOSHIFT
 #define DT_NOSHIFT 0
 #endif
+// DT_FEATURES: the scene features a build handles (dt_scene_dev.h: bit t for shape type t,
+// DT_FEAT_SPHL sphere lights, DT_FEAT_ON Oren-Nayar materials). A build without some of them has
+// those cases compiled out; dt_api.cpp launches it only for scenes whose feature mask it covers.
+#ifndef DT_FEATURES
+#define DT_FEATURES 0xFFFFu
+#endif
+#define DT_HAS(bit) (((DT_FEATURES) >> (bit)) & 1u)
+#define DT_NEED(bit) do { if (!DT_HAS(bit)) __builtin_unreachable(); } while (0)
+#define DT_ROOM_BUILD ((DT_FEATURES) == DT_ROOM_FEATURES)
+// the trace-kernel builds (Makefile): work sharing, RectPrismWithCylinder, and the product kernels
+// at 5 and 4 waves per SIMD: still frames of room scenes (C2, C3, C5's room frames), still frames
+// of any scene (*_full: C4's meshes), frames with motion-blur shifts (*_blur)
 #if DT_WITH_RPC
 #define DT_TRACE_KERNEL dt_trace_kernel_rpc
-#elif DT_W5 && DT_NOSHIFT
-#define DT_TRACE_KERNEL dt_trace_kernel_w5
-#elif DT_W5
-#define DT_TRACE_KERNEL dt_trace_kernel_w5_blur
 #elif DT_DONATE
 #define DT_TRACE_KERNEL dt_trace_kernel_dn
-#elif DT_NOSHIFT
+#elif DT_W5 && DT_NOSHIFT && DT_ROOM_BUILD
+#define DT_TRACE_KERNEL dt_trace_kernel_w5
+#elif DT_W5 && DT_NOSHIFT
+#define DT_TRACE_KERNEL dt_trace_kernel_w5_full
+#elif DT_W5
+#define DT_TRACE_KERNEL dt_trace_kernel_w5_blur
+#elif DT_NOSHIFT && DT_ROOM_BUILD
 #define DT_TRACE_KERNEL dt_trace_kernel
+#elif DT_NOSHIFT
+#define DT_TRACE_KERNEL dt_trace_kernel_full
 #else
 #define DT_TRACE_KERNEL dt_trace_kernel_blur
 #endif
-// the 4-wave still build also carries the small kernels and the launch-record helpers
-#define DT_HELPERS (!DT_WITH_RPC && !DT_DONATE && !DT_ISECT && !DT_W5 && DT_NOSHIFT)
+// the 4-wave room build also carries the small kernels and the launch-record helpers
+#define DT_HELPERS (!DT_WITH_RPC && !DT_DONATE && !DT_ISECT && !DT_W5 && DT_NOSHIFT && DT_ROOM_BUILD)
 
 #define DT_STACK_MAX 48
 #define DT_MAX_CLOUD_STEPS 2048
@@ -821,11 +837,13 @@ __device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, GP
   ccol = -1;
   switch (type) {
     case DT_SHAPE_SPHERE:
+      DT_NEED(DT_SHAPE_SPHERE);
       return sphere_hit(g, ray, start, t, inside);
     case DT_SHAPE_CYLINDER:
     case DT_SHAPE_CHECKER_CYLINDER:
       return cyl_hit(g, ray, start, t, inside);
     case DT_SHAPE_TRIANGLE: {
+      DT_NEED(DT_SHAPE_TRIANGLE);
       inside = 0;
       float tf;
       if (!tri_core(g, ray, start, tf)) return false;
@@ -869,6 +887,8 @@ __device__ bool shape_hit(const DScene& S, int sid, int type, uint32_t flags, GP
       return rpc_hit(g, ray, start, t, inside, ccol);
 #endif
     case DT_SHAPE_CHECKERBOARD:
+      DT_NEED(DT_SHAPE_CHECKERBOARD);
+      [[fallthrough]];
     case DT_SHAPE_CHECKERBOARD_HOLE: {
       inside = 0;
       if (dot(G3(g, CK_GN), ray) == 0) {
@@ -917,11 +937,13 @@ __device__ bool shape_shadow(int type, uint32_t flags, GP g, V3 ray, V3 start,
   float tt, a, b;
   switch (type) {
     case DT_SHAPE_SPHERE:
+      DT_NEED(DT_SHAPE_SPHERE);
       return sphere_shadow(g, ray, start, t_max);
     case DT_SHAPE_CYLINDER:
     case DT_SHAPE_CHECKER_CYLINDER:
       return cyl_shadow(g, ray, start, t_max);
     case DT_SHAPE_TRIANGLE: {
+      DT_NEED(DT_SHAPE_TRIANGLE);
       float tf;
       if (!tri_core(g, ray, start, tf)) return false;
       return tf > 0.001 && tf < t_max;
@@ -936,6 +958,7 @@ __device__ bool shape_shadow(int type, uint32_t flags, GP g, V3 ray, V3 start,
       }
       return rect_hit_R(g + RC_R, ray, start, 1e-4f, tt, a, b, t_max) && tt < t_max;
     case DT_SHAPE_CHECKERBOARD:
+      DT_NEED(DT_SHAPE_CHECKERBOARD);
       return rect_hit_R(g + CK_R, ray, start, 1e-4f, tt, a, b, t_max) && tt < t_max;
     case DT_SHAPE_RECTPRISM_V2:
 #pragma unroll 1
@@ -983,6 +1006,7 @@ __device__ __forceinline__ V3 shape_norm(int type, uint32_t flags, GP g, V3 p, f
     }
 #endif
     case DT_SHAPE_SPHERE: {
+      DT_NEED(DT_SHAPE_SPHERE);
       V3 n = sub(p, G3(g, SP_C));
       return divs(n, norm(n));
     }
@@ -993,6 +1017,7 @@ __device__ __forceinline__ V3 shape_norm(int type, uint32_t flags, GP g, V3 p, f
       return normalized(sub(pc, mul(dot(pc, axis), axis)));
     }
     case DT_SHAPE_TRIANGLE:
+      DT_NEED(DT_SHAPE_TRIANGLE);
       return normalized(cross(G3(g, TR_R1), G3(g, TR_R2)));
     case DT_SHAPE_RECTANGLE: {
       V3 A, B, C, D;
@@ -1063,6 +1088,7 @@ __device__ __forceinline__ int shape_uv(int type, uint32_t flags, GP g, V3 p, fl
       return 1;
     }
     case DT_SHAPE_TRIANGLE: {
+      DT_NEED(DT_SHAPE_TRIANGLE);
       V3 A = G3(g, TR_A), B = G3(g, TR_B), C = G3(g, TR_C);
       V3 n = cross(sub(B, A), sub(C, A));
       V3 n_a = cross(sub(C, B), sub(p, B));
@@ -1944,6 +1970,7 @@ __device__ __forceinline__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L,
     }
     return sub(rect_sample_f(v3a(L.A), v3a(L.B), v3a(L.D), f01(w0), f01(w1)), point);
   }
+  DT_NEED(DT_FEAT_SPHL);
   return sphere_light_sample(c, L, li, point, node, st_sphl);
 }
 
@@ -1962,6 +1989,7 @@ __device__ __forceinline__ V3 brdf(const DParams& P, const DMat& M, const DT_CAS
   V3 ray_col;
   const float roughness = M.roughness;
   if (M.model == DT_MODEL_OREN_NAYAR) {
+    DT_NEED(DT_FEAT_ON);
     const float A = M.on_a, B = M.on_b;   // per material (host, cpp:896-897)
     float vn = (float)dot(e_dir, normal);
     float ln = (float)dot(sn, normal);
@@ -3126,11 +3154,6 @@ extern "C" size_t dt_launch_size(void) { return sizeof(DLaunch); }
 extern "C" size_t dt_scene_struct_offset(void) { return offsetof(DLaunch, S); }
 extern "C" size_t dt_params_struct_offset(void) { return offsetof(DLaunch, P); }
 
-extern "C" hipError_t dt_launch_trace(const void* dev_launch, float* out, int grid, hipStream_t stream)
-{
-  hipLaunchKernelGGL(dt_trace_kernel, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
-  return hipGetLastError();
-}
 extern "C" hipError_t dt_launch_sky_miss(const void* dev_launch, float* out, int64_t n_px, hipStream_t stream)
 {
   int64_t blocks = (n_px + 255) / 256;
@@ -3152,43 +3175,19 @@ extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_
                      world, slab_floats, slabs, image);
   return hipGetLastError();
 }
-extern "C" const void* dt_trace_kernel_ptr(void) { return (const void*)dt_trace_kernel; }
-#elif DT_ISECT
-#elif DT_W5 && DT_NOSHIFT   // the trace kernel at 5 waves per SIMD
-static_assert(DT_TRACE_MIN_WAVES == 5 && DT_PSUM_LDS == 2, "dt_kernels_w5.o: Makefile flags");
-extern "C" hipError_t dt_launch_trace_w5(const void* dev_launch, float* out, int grid, hipStream_t stream)
+#endif
+
+#if !DT_ISECT
+// every trace-kernel build: <kernel>_launch and <kernel>_ptr (dt_api.cpp's kernel table)
+#define DT_CAT2(a, b) a##b
+#define DT_CAT(a, b) DT_CAT2(a, b)
+#if DT_W5
+static_assert(DT_TRACE_MIN_WAVES == 5 && DT_PSUM_LDS == 2, "5-wave build: Makefile W5FLAGS");
+#endif
+extern "C" hipError_t DT_CAT(DT_TRACE_KERNEL, _launch)(const void* dev_launch, float* out, int grid, hipStream_t stream)
 {
-  hipLaunchKernelGGL(dt_trace_kernel_w5, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
+  hipLaunchKernelGGL(DT_TRACE_KERNEL, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
   return hipGetLastError();
 }
-extern "C" const void* dt_trace_kernel_w5_ptr(void) { return (const void*)dt_trace_kernel_w5; }
-#elif DT_W5   // the same with motion-blur shifts
-static_assert(DT_TRACE_MIN_WAVES == 5 && DT_PSUM_LDS == 2, "dt_kernels_w5_blur.o: Makefile flags");
-extern "C" hipError_t dt_launch_trace_w5_blur(const void* dev_launch, float* out, int grid, hipStream_t stream)
-{
-  hipLaunchKernelGGL(dt_trace_kernel_w5_blur, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
-  return hipGetLastError();
-}
-extern "C" const void* dt_trace_kernel_w5_blur_ptr(void) { return (const void*)dt_trace_kernel_w5_blur; }
-#elif DT_DONATE   // the trace kernel with DFS work sharing inside the wave
-extern "C" hipError_t dt_launch_trace_dn(const void* dev_launch, float* out, int grid, hipStream_t stream)
-{
-  hipLaunchKernelGGL(dt_trace_kernel_dn, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
-  return hipGetLastError();
-}
-extern "C" const void* dt_trace_kernel_dn_ptr(void) { return (const void*)dt_trace_kernel_dn; }
-#elif !DT_WITH_RPC   // the 4-wave trace kernel with motion-blur shifts
-extern "C" hipError_t dt_launch_trace_blur(const void* dev_launch, float* out, int grid, hipStream_t stream)
-{
-  hipLaunchKernelGGL(dt_trace_kernel_blur, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
-  return hipGetLastError();
-}
-extern "C" const void* dt_trace_kernel_blur_ptr(void) { return (const void*)dt_trace_kernel_blur; }
-#else   // DT_WITH_RPC: the trace kernel for scenes with a RectPrismWithCylinder
-extern "C" hipError_t dt_launch_trace_rpc(const void* dev_launch, float* out, int grid, hipStream_t stream)
-{
-  hipLaunchKernelGGL(dt_trace_kernel_rpc, dim3(grid), dim3(64), 0, stream, (const DLaunch*)dev_launch, out);
-  return hipGetLastError();
-}
-extern "C" const void* dt_trace_kernel_rpc_ptr(void) { return (const void*)dt_trace_kernel_rpc; }
+extern "C" const void* DT_CAT(DT_TRACE_KERNEL, _ptr)(void) { return (const void*)DT_TRACE_KERNEL; }
 #endif

@@ -80,14 +80,16 @@ BLUR_CASES = [  # (id, builder args, frame, tile world): still frames, 5-wave (6
     ("c3_1of64_w5", ("final", 240, 0, 1920, 1080, 64, 8), 240, 64),
     ("c2_full_w4", ("final", 240, 0, 800, 600, 16, 4), 240, 1),
     ("c5_room_480_1of512_w5", ("final", 480, 0, 3840, 2160, 64, 10), 480, 512),
+    ("c4_models_1of256_w5_full", ("final", 240, 1, 1920, 1080, 256, 8), 240, 256),
 ]
 
 
 @pytest.mark.parametrize("case", BLUR_CASES, ids=[c[0] for c in BLUR_CASES])
 def test_still_kernels_match_blur_builds(cuda, monkeypatch, case):
     """Frames below frame_prism take the product kernels built without the motion-blur shift paths
-    (dt_kernels.hip DT_NOSHIFT); DT_BLUR_KERNEL=1 renders them with the *_blur builds, which every
-    later frame takes. Same rays, same bits."""
+    (dt_kernels.hip DT_NOSHIFT): the room builds for scenes within DT_ROOM_FEATURES, the *_full
+    builds otherwise (C4's meshes: triangles, Oren-Nayar). DT_BLUR_KERNEL=1 renders them with the
+    *_blur builds, which every later frame takes. Same rays, same bits."""
     label, args, frame, world = case
     g, built = _globals(*args)
     tile = dt.tiles(rank=0, world=world, layout=dt.DT_OUT_SLAB) if world > 1 else dt.tiles()
