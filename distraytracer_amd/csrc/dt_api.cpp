@@ -297,6 +297,8 @@ int dt_scene_prepare(const dt_scene_desc* desc, const dt_globals* g, dt_scene** 
       const int t = desc->shapes[i].type;
       feat |= (t >= 0 && t < DT_FEAT_SPHL) ? 1u << t : 1u << 31;
       if (desc->shapes[i].model == DT_MODEL_OREN_NAYAR) feat |= 1u << DT_FEAT_ON;
+      if (desc->shapes[i].material == DT_MAT_GLASS) feat |= 1u << DT_FEAT_GLASS;
+      if (desc->shapes[i].emit == DT_EMIT_SPHERE) feat |= 1u << DT_FEAT_SPHL;
     }
     for (int i = 0; i < desc->n_lights; ++i) {
       const int t = desc->lights[i].type;
@@ -757,6 +759,10 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
     PL.sky_defer = 1;
     hs.sky_miss = sc->d_sky_miss;
   }
+  // DT_GENERAL_WALKS=1: every wave takes the exact reference-tree walks that axis-parallel rays
+  // take (the tests' check of those rare, out-of-line paths against the product walks)
+  const char* gw_env = getenv("DT_GENERAL_WALKS");
+  if (gw_env && gw_env[0] == '1') PL.boxes_ordered = 0;
   PL.donate = donate ? 1 : 0;
   const char* dn_after = getenv("DT_DONATE_AFTER");
   PL.donate_after = dn_after ? atoi(dn_after) : 2;

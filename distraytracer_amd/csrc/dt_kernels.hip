@@ -94,7 +94,7 @@ using namespace dtd;
 #define DT_NOSHIFT 0
 #endif
 // DT_FEATURES: the scene features a build handles (dt_scene_dev.h: bit t for shape type t,
-// DT_FEAT_SPHL sphere lights, DT_FEAT_ON Oren-Nayar materials). A build without some of them has
+// DT_FEAT_SPHL sphere lights and emitters, DT_FEAT_ON Oren-Nayar, DT_FEAT_GLASS refraction). A build without some of them has
 // those cases compiled out; dt_api.cpp launches it only for scenes whose feature mask it covers.
 #ifndef DT_FEATURES
 #define DT_FEATURES 0xFFFFu
@@ -1525,13 +1525,61 @@ __device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams
   return any;
 }
 
+// The exact walks on the reference tree for waves with an axis-parallel or NaN ray (MODE 1) are
+// rare in the still builds (never taken for motion blur there): called out of line (DT_GENERAL_OOL),
+// so their code does not shape the register allocation of the hot walks. Records go by value both ways, so no
+// address of the caller's hit record or counters escapes into memory.
+// Out of line in the 4-wave still builds only: C2 +5%, but the 5-wave build (96 VGPRs) loses 7.5% on
+// C3 to the call's register save/restore (profiles/r04r_ab_general_ool.log)
+#ifndef DT_GENERAL_OOL
+#define DT_GENERAL_OOL (DT_NOSHIFT && !DT_W5)
+#endif
+template <class CNT>
+struct GeneralHit {
+  HitRec h;
+  CNT cnt;
+  bool any;
+};
+template <class CNT>
+__device__ __noinline__ GeneralHit<CNT> closest_hit_general(const DScene* S, const DParams* P, Walk w, bool active,
+                                                            V3 ray, V3 org, HitRec h, CNT cnt)
+{
+  GeneralHit<CNT> o;
+  o.any = closest_hit_walk<1>(*S, *P, w, active, ray, org, 0.0f, h, cnt);
+  o.h = h;
+  o.cnt = cnt;
+  return o;
+}
+template <class CNT>
+struct GeneralOcc {
+  CNT cnt;
+  bool occl;
+};
+template <class CNT>
+__device__ __noinline__ GeneralOcc<CNT> occluded_general(const DScene* S, const DParams* P, Walk w, bool active,
+                                                         V3 bstart, V3 sn, V3 sstart, float t_max, int skip_shape,
+                                                         CNT cnt);
+template <class CNT>
+__device__ __forceinline__ bool closest_hit_exact(const DScene& S, const DParams& P, const Walk& w, bool active, V3 ray,
+                                                  V3 org, float shift, HitRec& h, CNT& cnt)
+{
+#if DT_GENERAL_OOL
+  const GeneralHit<CNT> o = closest_hit_general(&S, &P, w, active, ray, org, h, cnt);
+  h = o.h;
+  cnt = o.cnt;
+  return o.any;
+#else
+  return closest_hit_walk<1>(S, P, w, active, ray, org, shift, h, cnt);
+#endif
+}
+
 template <class CNT>
 __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, bool active, V3 ray, V3 org, float shift,
                                             HitRec& h, CNT& cnt, int pblock = -1)
 {
   const Walk w = make_walk(P, active, ray, org, shift);
   if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift)))
-    return closest_hit_walk<1>(S, P, w, active, ray, org, shift, h, cnt);
+    return closest_hit_exact(S, P, w, active, ray, org, shift, h, cnt);
   bool any;
   if (pblock >= 0 && (!w.bump_wave || P.pl_bump)) {
     // blur passes take the bump tree's lists, stored after the pass-0 lists
@@ -1547,7 +1595,7 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
   // reproduces it, so with the alternative trees such waves (never seen in practice) repeat the
   // walk on the reference tree
   if ((w.bump_wave || (P.n_fnodes > 0 && (P.ftree_mode & 1))) && __ballot(h.edge))
-    return closest_hit_walk<1>(S, P, w, active, ray, org, shift, h, cnt);
+    return closest_hit_exact(S, P, w, active, ray, org, shift, h, cnt);
   return any;
 }
 
@@ -1743,6 +1791,17 @@ __device__ __forceinline__ void sg_coords(const DParams& P, V3 p, float& x, floa
 }
 
 template <class CNT>
+__device__ __noinline__ GeneralOcc<CNT> occluded_general(const DScene* S, const DParams* P, Walk w, bool active,
+                                                         V3 bstart, V3 sn, V3 sstart, float t_max, int skip_shape,
+                                                         CNT cnt)
+{
+  GeneralOcc<CNT> o;
+  o.occl = occluded_walk<1>(*S, *P, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, cnt);
+  o.cnt = cnt;
+  return o;
+}
+
+template <class CNT>
 __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
                                          V3 sstart, float t_max, int skip_shape, int li, float shift, CNT& cnt)
 {
@@ -1750,8 +1809,15 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
 #ifdef DT_STAMPS
   cnt.cur_path = 2;
 #endif
-  if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift)))
+  if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift))) {
+#if DT_GENERAL_OOL
+    const GeneralOcc<CNT> o = occluded_general(&S, &P, w, active, bstart, sn, sstart, t_max, skip_shape, cnt);
+    cnt = o.cnt;
+    return o.occl;
+#else
     return occluded_walk<1>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+#endif
+  }
   // blur passes use the grid when its lists were built for their shifts (sg_ypad)
   // (umbra cells are only proven for shifts >= 0: with symmetric padding blur waves walk the tree)
   const bool bump_list = w.bump_wave && P.sg_ypad >= P.bump_pad && P.bump_up_only;
@@ -2410,7 +2476,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
           int nref = 0;
           if (rn <= 0) atomicAdd(S.stats + ST_REFL, 1ull);
           else if (rn > eps) nref = (glossy && !P.nogloss) ? P.brdf_samples : 1;
-          const bool glass = M.material == DT_MAT_GLASS;
+          const bool glass = DT_HAS(DT_FEAT_GLASS) && M.material == DT_MAT_GLASS;
           const int base = sp;
           if (base + nref + (glass ? 1 : 0) > DT_STACK_MAX) {
             atomicAdd(S.stats + ST_STACK, 1ull);
@@ -2507,7 +2573,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
       // emissive (cpp:775-789)
       if (M.flags & DT_F_LIGHT) {
         DT_WK(DT_WK_EMIT, true);
-        if (M.emit == DT_EMIT_SPHERE) {
+        if (DT_HAS(DT_FEAT_SPHL) && M.emit == DT_EMIT_SPHERE) {
           float hitdot = (float)dot(in, normalized(sub(v3a(M.center), isectP)));
           double f = (0.1 * pw1((double)hitdot) + 0.05 * pw5((double)hitdot)) + 0.9;
           own = mul(f, mul(k, shape_color));
@@ -2528,11 +2594,8 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
     DT_T(t3);
     DT_ACC(2, t2, t3);
     // ---- direct lighting (cpp:800-959) ------------------------------------------------
-    // Two passes over the lights. Pass 1 walks one packet shadow ray per light and keeps only
-    // a visibility bit; the shading inputs (normal, eye, colour) are parked in LDS meanwhile,
-    // so the walks run with a small live register set instead of spilling the BRDF state to
-    // scratch around every walk. Pass 2 regenerates each unoccluded light sample (counter RNG:
-    // the same values) and evaluates the BRDFs in light order, as the reference's loop does.
+    // One packet shadow walk per light; the shading inputs (normal, eye, colour) are parked in
+    // LDS across the walks so they run with a small live register set (the loop below).
     if (__ballot(shade)) {
       // getUV/texel depend only on the hit point: once per node (the reference repeats them
       // per unoccluded light with the same result). UV type 0 makes the node's own light 0

@@ -99,3 +99,27 @@ def test_still_kernels_match_blur_builds(cuda, monkeypatch, case):
     blur, st1 = _render(g, built, frame, tile, False, monkeypatch)
     assert st0.rays == st1.rays and st0.shadow_rays == st1.shadow_rays
     log_equal("%s still kernel vs blur build (bits)" % label, still.view(np.uint32), blur.view(np.uint32))
+
+
+GENERAL_CASES = [  # (id, builder args, frame, tile world)
+    ("c2_full_w4_room", ("final", 240, 0, 800, 600, 16, 4), 240, 1),
+    ("c4_16spp_1of64_w4_full", ("final", 240, 1, 1920, 1080, 16, 8), 240, 64),
+    ("c3_1of64_w5", ("final", 240, 0, 1920, 1080, 64, 8), 240, 64),
+]
+
+
+@pytest.mark.parametrize("case", GENERAL_CASES, ids=[c[0] for c in GENERAL_CASES])
+def test_general_walks_match_product_walks(cuda, monkeypatch, case):
+    """DT_GENERAL_WALKS=1 sends every wave down the exact reference-tree walks that only waves with
+    an axis-parallel or NaN ray take otherwise (called out of line in the 4-wave still builds,
+    dt_kernels.hip DT_GENERAL_OOL). The gathered leaves and tie order are the reference's either
+    way, so the image is the same bit for bit with the same rays."""
+    label, args, frame, world = case
+    g, built = _globals(*args)
+    tile = dt.tiles(rank=0, world=world, layout=dt.DT_OUT_SLAB) if world > 1 else dt.tiles()
+    monkeypatch.setenv("DT_GENERAL_WALKS", "0")
+    base, st0 = _render(g, built, frame, tile, False, monkeypatch)
+    monkeypatch.setenv("DT_GENERAL_WALKS", "1")
+    gen, st1 = _render(g, built, frame, tile, False, monkeypatch)
+    assert st0.rays == st1.rays and st0.shadow_rays == st1.shadow_rays
+    log_equal("%s general walks vs product walks (bits)" % label, gen.view(np.uint32), base.view(np.uint32))
