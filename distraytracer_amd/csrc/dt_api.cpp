@@ -27,13 +27,16 @@ extern "C" hipError_t dt_launch_normalize(const double* in, double* out, int64_t
 // the trace-kernel builds (dt_kernels.hip DT_TRACE_KERNEL, Makefile TRACE_BUILDS)
 #define DT_TRACE_BUILD(k)                                                                              \
   extern "C" hipError_t k##_launch(const void* dev_launch, float* out, int grid, hipStream_t stream); \
-  extern "C" const void* k##_ptr(void);
+  extern "C" const void* k##_ptr(void);                                                                \
+  extern "C" int k##_traits(void);
 DT_TRACE_BUILD(dt_trace_kernel)
 DT_TRACE_BUILD(dt_trace_kernel_full)
 DT_TRACE_BUILD(dt_trace_kernel_blur)
 DT_TRACE_BUILD(dt_trace_kernel_w5)
 DT_TRACE_BUILD(dt_trace_kernel_w5_full)
 DT_TRACE_BUILD(dt_trace_kernel_w5_blur)
+DT_TRACE_BUILD(dt_trace_kernel_sky)
+DT_TRACE_BUILD(dt_trace_kernel_w5_sky)
 DT_TRACE_BUILD(dt_trace_kernel_dn)
 DT_TRACE_BUILD(dt_trace_kernel_rpc)
 #undef DT_TRACE_BUILD
@@ -66,6 +69,8 @@ struct HScene {
   const uint32_t* pl_list;
   uint8_t* sky_miss;
   void* dn_pool;
+  uint32_t* again_list;
+  unsigned int* again_n;
 };
 
 #define DT_N_STAMPS (64 + 3 * 8 * 256)   // diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters):
@@ -183,6 +188,14 @@ struct dt_scene {
   std::vector<double> pl_key;
   uint8_t* d_sky_miss = nullptr;   // 1-spp launches: missed-pixel flags (dt_sky_miss_kernel clears them)
   int64_t sky_miss_cap = 0;
+  // sky items (dt_kernels.hip DT_SKY_AGAIN): the list a still build leaves to its *_sky build, that
+  // launch's record (pinned staging h_launch2, guarded by ev_copy like h_launch) and its counters
+  uint32_t* d_again = nullptr;
+  int64_t again_cap = 0;
+  void* d_launch2 = nullptr;
+  uint8_t* h_launch2 = nullptr;
+  unsigned long long* d_stats2 = nullptr;   // ST_N counters + queue word + list count
+  bool again_used = false;                  // the last render ran the second launch
   void* d_dn_pool = nullptr;       // dt_trace_kernel_dn: DT_DN_POOL_REC work-sharing records per wave
   int64_t dn_pool_waves = 0;
   PrimLists pl;
@@ -352,7 +365,8 @@ static void release_device(dt_scene* s)
 {
   void** bufs[] = {&s->d_pl_cells, &s->d_pl_list, &s->d_nodes, &s->d_fnodes, &s->d_bnodes, &s->d_bparent,
                    &s->d_sg_cells, &s->d_sg_list, &s->d_leaf, &s->d_hdr, &s->d_geom, &s->d_mat, &s->d_lights,
-                   &s->d_tex, &s->d_zs, (void**)&s->d_stats, &s->d_launch, (void**)&s->d_sky_miss, &s->d_dn_pool};
+                   &s->d_tex, &s->d_zs, (void**)&s->d_stats, &s->d_launch, (void**)&s->d_sky_miss, &s->d_dn_pool,
+                   (void**)&s->d_again, &s->d_launch2, (void**)&s->d_stats2};
   for (void** b : bufs) {
     if (*b) (void)hipFree(*b);
     *b = nullptr;
@@ -362,8 +376,12 @@ static void release_device(dt_scene* s)
     *e = nullptr;
   }
   if (s->h_launch) (void)hipHostFree(s->h_launch);
+  if (s->h_launch2) (void)hipHostFree(s->h_launch2);
   if (s->h_zs) (void)hipHostFree(s->h_zs);
   s->h_launch = nullptr;
+  s->h_launch2 = nullptr;
+  s->again_cap = 0;
+  s->again_used = false;
   s->h_zs = nullptr;
   s->zs_cap = 0;
   s->sky_miss_cap = 0;
@@ -701,15 +719,21 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   // against each other)
   const char* bk_env = getenv("DT_BLUR_KERNEL");
   const bool blur = P.frame >= P.frame_prism || (bk_env && bk_env[0] == '1');
-  struct Build { hipError_t (*launch)(const void*, float*, int, hipStream_t); const void* (*ptr)(void); int resident; };
-  static Build builds[8] = {
-      {dt_trace_kernel_launch, dt_trace_kernel_ptr, 0},           {dt_trace_kernel_full_launch, dt_trace_kernel_full_ptr, 0},
-      {dt_trace_kernel_blur_launch, dt_trace_kernel_blur_ptr, 0}, {dt_trace_kernel_w5_launch, dt_trace_kernel_w5_ptr, 0},
-      {dt_trace_kernel_w5_full_launch, dt_trace_kernel_w5_full_ptr, 0},
-      {dt_trace_kernel_w5_blur_launch, dt_trace_kernel_w5_blur_ptr, 0},
-      {dt_trace_kernel_dn_launch, dt_trace_kernel_dn_ptr, 0},     {dt_trace_kernel_rpc_launch, dt_trace_kernel_rpc_ptr, 0}};
+  struct Build {
+    hipError_t (*launch)(const void*, float*, int, hipStream_t);
+    const void* (*ptr)(void);
+    int (*traits)(void);
+    int resident;
+  };
+#define DT_B(k) {k##_launch, k##_ptr, k##_traits, 0}
+  static Build builds[10] = {DT_B(dt_trace_kernel),    DT_B(dt_trace_kernel_full),    DT_B(dt_trace_kernel_blur),
+                             DT_B(dt_trace_kernel_w5), DT_B(dt_trace_kernel_w5_full), DT_B(dt_trace_kernel_w5_blur),
+                             DT_B(dt_trace_kernel_dn), DT_B(dt_trace_kernel_rpc),   DT_B(dt_trace_kernel_sky),
+                             DT_B(dt_trace_kernel_w5_sky)};
+#undef DT_B
   const int variant = blur ? 2 : sc->room ? 0 : 1;
   Build& kb = sc->no_cull ? builds[7] : donate ? builds[6] : builds[(w5 ? 3 : 0) + variant];
+  Build& kb2 = builds[w5 ? 9 : 8];   // the *_sky build of the same wave count: renders the sky items
   if (!kb.resident) kb.resident = max_resident_waves(kb.ptr(), 64);
   const int64_t waves = kb.resident;
   int64_t grid = P.n_items < waves ? P.n_items : waves;
@@ -763,6 +787,31 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   // take (the tests' check of those rare, out-of-line paths against the product walks)
   const char* gw_env = getenv("DT_GENERAL_WALKS");
   if (gw_env && gw_env[0] == '1') PL.boxes_ordered = 0;
+  // a still build without the sky march lists its items with a missed sample (multi-sample
+  // renders of a scene with perlin_cloud; dt_kernels.hip DT_SKY_AGAIN) and the *_sky build of the
+  // same wave count renders them in a second launch, with its own counters: the first launch
+  // already counted their rays and abort conditions, the second adds only their sky and NaN
+  // pixels (dt_collect_stats)
+  const bool again = (kb.traits() & 1) && PL.perlin_cloud && !PL.sky_defer;
+  PL.sky_again = again ? 1 : 0;
+  hs.again_list = nullptr;
+  hs.again_n = nullptr;
+  if (again) {
+    if (!sc->d_stats2) {
+      HIPCHK(hipMalloc((void**)&sc->d_stats2, sizeof(unsigned long long) * (ST_N + 2)));
+      HIPCHK(hipMalloc(&sc->d_launch2, dt_launch_size()));
+      HIPCHK(hipHostMalloc((void**)&sc->h_launch2, dt_launch_size(), hipHostMallocDefault));
+    }
+    if (PL.n_items > sc->again_cap) {
+      HIPCHK(hipStreamSynchronize(st));
+      if (sc->d_again) (void)hipFree(sc->d_again);
+      sc->d_again = nullptr;
+      HIPCHK(hipMalloc((void**)&sc->d_again, sizeof(uint32_t) * PL.n_items));
+      sc->again_cap = PL.n_items;
+    }
+    hs.again_list = sc->d_again;
+    hs.again_n = (unsigned int*)(sc->d_stats2 + ST_N + 1);
+  }
   PL.donate = donate ? 1 : 0;
   const char* dn_after = getenv("DT_DONATE_AFTER");
   PL.donate_after = dn_after ? atoi(dn_after) : 2;
@@ -771,11 +820,30 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   memcpy(sc->h_launch + dt_params_struct_offset(), &PL, sizeof(PL));
   if (nz) HIPCHK(hipMemcpyAsync(sc->d_zs, sc->h_zs, nz * sizeof(float), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(sc->d_launch, sc->h_launch, dt_launch_size(), hipMemcpyHostToDevice, st));
+  if (again) {   // the second launch: the listed items, counters of its own
+    HScene hs2 = hs;
+    hs2.stats = sc->d_stats2;
+    hs2.queue = sc->d_stats2 + ST_N;
+    dtd::DParams PL2 = PL;
+    PL2.sky_again = 2;
+    PL2.item_batch = 1;
+    PL2.prio_steps = 0;
+    memset(sc->h_launch2, 0, dt_launch_size());
+    memcpy(sc->h_launch2 + dt_scene_struct_offset(), &hs2, sizeof(hs2));
+    memcpy(sc->h_launch2 + dt_params_struct_offset(), &PL2, sizeof(PL2));
+    HIPCHK(hipMemcpyAsync(sc->d_launch2, sc->h_launch2, dt_launch_size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(sc->d_stats2, 0, sizeof(unsigned long long) * (ST_N + 2), st));
+  }
   HIPCHK(hipEventRecord(sc->ev_copy, st));
   sc->copy_pending = true;
   HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 1 + DT_N_STAMPS), st));
   HIPCHK(hipEventRecord(sc->ev0, st));
   HIPCHK(kb.launch(sc->d_launch, out_dev, (int)grid, st));
+  if (again) {
+    if (!kb2.resident) kb2.resident = max_resident_waves(kb2.ptr(), 64);
+    HIPCHK(kb2.launch(sc->d_launch2, out_dev, (int)(grid < kb2.resident ? grid : kb2.resident), st));
+  }
+  sc->again_used = again;
   if (PL.sky_defer) HIPCHK(dt_launch_sky_miss(sc->d_launch, out_dev, n_px, st));
   HIPCHK(hipEventRecord(sc->ev1, st));
   sc->timed = true;
@@ -794,6 +862,12 @@ int dt_collect_stats(const dt_scene* sc_c, void* stream, dt_stats* stats)
   if (!stats) return DT_OK;
   unsigned long long h[ST_N];
   HIPCHK(hipMemcpy(h, sc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  if (sc->again_used) {   // the sky items' second launch: their sky and NaN pixels
+    unsigned long long h2[ST_N];
+    HIPCHK(hipMemcpy(h2, sc->d_stats2, sizeof(h2), hipMemcpyDeviceToHost));
+    h[ST_SKY] += h2[ST_SKY];
+    h[ST_NAN] += h2[ST_NAN];
+  }
   memset(stats, 0, sizeof(*stats));
   const dtd::DParams& P = sc->last;
   int64_t px = 0;

@@ -93,6 +93,21 @@ using namespace dtd;
 #ifndef DT_NOSHIFT
 #define DT_NOSHIFT 0
 #endif
+// DT_SKY_AGAIN: the still builds carry no cooperative sky march (its noise code took ~95 of the
+// 5-wave build's 133 spilled VGPRs). A multi-sample item with a missed sample is listed instead of
+// stored, and a second launch of the *_sky build of the same wave count (DT_SKY_BUILD: still frames,
+// every feature, the march; its queue runs over the list, DT_AGAIN_QUEUE) renders the listed items
+// again from the same counter-RNG draws (dt_api.cpp enqueue_render; P.sky_again). Room scenes never
+// miss. Diagnostic builds (work counters, stamps) keep the march so their counts stay one launch's.
+#ifndef DT_SKY_BUILD
+#define DT_SKY_BUILD 0
+#endif
+#if DT_NOSHIFT && !DT_SKY_BUILD && !defined(DT_WORK_COUNTERS) && !defined(DT_STAMPS)
+#define DT_SKY_AGAIN 1
+#else
+#define DT_SKY_AGAIN 0
+#endif
+#define DT_AGAIN_QUEUE DT_SKY_BUILD
 // DT_FEATURES: the scene features a build handles (dt_scene_dev.h: bit t for shape type t,
 // DT_FEAT_SPHL sphere lights and emitters, DT_FEAT_ON Oren-Nayar, DT_FEAT_GLASS refraction). A build without some of them has
 // those cases compiled out; dt_api.cpp launches it only for scenes whose feature mask it covers.
@@ -109,6 +124,10 @@ using namespace dtd;
 #define DT_TRACE_KERNEL dt_trace_kernel_rpc
 #elif DT_DONATE
 #define DT_TRACE_KERNEL dt_trace_kernel_dn
+#elif DT_W5 && DT_SKY_BUILD
+#define DT_TRACE_KERNEL dt_trace_kernel_w5_sky
+#elif DT_SKY_BUILD
+#define DT_TRACE_KERNEL dt_trace_kernel_sky
 #elif DT_W5 && DT_NOSHIFT && DT_ROOM_BUILD
 #define DT_TRACE_KERNEL dt_trace_kernel_w5
 #elif DT_W5 && DT_NOSHIFT
@@ -182,6 +201,8 @@ struct DScene {
   const uint32_t* pl_list;  // (fast-tree node, float bits of t_near) per entry
   uint8_t* sky_miss;        // P.sky_defer: per queue position, 1 when the pixel's sample missed
   void* dn_pool;            // P.donate: DT_DN_POOL_REC records of 32 B per resident wave (DFS work sharing)
+  uint32_t* again_list;     // P.sky_again: the items a launch without the sky left to a launch with it
+  unsigned int* again_n;    // ... and their count
 };
 
 // pow(x, n) for the integer exponents the reference writes as pow(x, 2.0) etc. pow(x, 1) is x
@@ -2910,16 +2931,20 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   // of every wave is its own by block index: 5120 waves starting at once would otherwise queue
   // behind one another on the one atomic word; the shared counter hands out the items after them.
   const int batch = P.item_batch > 1 ? P.item_batch : 1;
-  int64_t item = (int64_t)blockIdx.x * batch, batch_end = item + batch;
+  // P.sky_again == 2: the queue runs over the items a launch without the sky listed
+  const int64_t n_queue = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)*S.again_n : P.n_items;
+  int64_t qpos = (int64_t)blockIdx.x * batch, batch_end = qpos + batch;
   while (true) {
-    if (item >= batch_end) {
+    if (qpos >= batch_end) {
       if (lane == 0) item_s = atomicAdd(S.queue, (unsigned long long)batch);
       __syncthreads();
-      item = (int64_t)item_s + (int64_t)gridDim.x * batch;
-      batch_end = item + batch;
+      qpos = (int64_t)item_s + (int64_t)gridDim.x * batch;
+      batch_end = qpos + batch;
       __syncthreads();
     }
-    if (item >= P.n_items) break;
+    if (qpos >= n_queue) break;
+    const int64_t item = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)S.again_list[qpos] : qpos;
+    bool sky_again = false;
 
     const int group = P.ppw;
     const int spp = P.spp;
@@ -2999,6 +3024,8 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       // P.sky_defer) flagged for dt_sky_miss_kernel
       if (P.sky_defer) {
         if (miss) S.sky_miss[item * group + j] = 1;
+      } else if (DT_SKY_AGAIN && P.perlin_cloud) {
+        if (__ballot(miss)) sky_again = true;   // rendered again by a build with the sky
       } else if (P.perlin_cloud) {
         for (int jj = 0; jj < group; ++jj) {
           if (__ballot(miss && j == jj)) {
@@ -3057,7 +3084,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       int64_t qo;
       bool qv;
       pixel_of(P, item * group + lane, qx, qy, qo, qv);
-      if (qv && !(P.sky_defer && S.sky_miss[item * group + lane])) {
+      if (qv && !sky_again && !(P.sky_defer && S.sky_miss[item * group + lane])) {
         V3 color = divs(v3(psum[0][lane], psum[1][lane], psum[2][lane]), spp);
 #ifdef DT_ITEM_TIMES   // diagnostic builds (tools/item_times.py): the item's wave cycles / 1e4, raw
         {
@@ -3071,8 +3098,9 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
       }
     }
+    if (sky_again && lane == 0) S.again_list[atomicAdd(S.again_n, 1u)] = (uint32_t)item;
     if (P.prio_steps > 0) __builtin_amdgcn_s_setprio(0);
-    ++item;
+    ++qpos;
   }
   {
     __syncthreads();
@@ -3253,4 +3281,6 @@ extern "C" hipError_t DT_CAT(DT_TRACE_KERNEL, _launch)(const void* dev_launch, f
   return hipGetLastError();
 }
 extern "C" const void* DT_CAT(DT_TRACE_KERNEL, _ptr)(void) { return (const void*)DT_TRACE_KERNEL; }
+// bit 0: the build lists sky items for another launch (DT_SKY_AGAIN)
+extern "C" int DT_CAT(DT_TRACE_KERNEL, _traits)(void) { return DT_SKY_AGAIN ? 1 : 0; }
 #endif

@@ -155,6 +155,9 @@ struct DParams {
   int32_t prio_steps;     // DFS steps after which a wave raises its issue priority (0: never)
   int32_t ls_first;       // first area (rectangle) light: where the light-sample cache starts
   int32_t sky_defer;      // 1 spp: missed pixels are flagged, dt_sky_miss_kernel marches them per lane
+  int32_t sky_again;      // builds without the in-kernel sky (DT_SKY_AGAIN): an item with a missed
+                          // sample is listed (DScene::again_list) instead of stored; 2: this launch
+                          // (a build with the sky) renders the listed items
   int32_t no_cull;        // 1: no t-culling of boxes (closest hit past the best t, shadow past the light):
                           // a RectPrismWithCylinder occludes beyond the light and its hole can be hit
                           // outside its box (host: no shadow grid, no primary lists either)

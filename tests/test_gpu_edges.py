@@ -135,3 +135,20 @@ def test_host_output_buffer_fully_written(cuda, aa, depth, builder, frame):
     if aa == 1:
         assert st.sky_pixels > 0
     assert_parity("host output buffer %dx%d aa=%d frame %d" % (g.xRes, g.yRes, aa, frame), out, ref)
+
+
+@pytest.mark.parametrize("W,H,aa,depth,world", [(48, 32, 4, 2, 1), (40, 24, 64, 3, 1), (64, 48, 16, 2, 3)])
+def test_sky_items_rendered_again(cuda, W, H, aa, depth, world):
+    """Still-frame builds carry no sky march (dt_kernels.hip DT_SKY_AGAIN): a multi-sample item with
+    a missed sample is listed and rendered again by the *_sky build in a second launch. The spheres
+    scene with perlin_cloud on has sky around the spheres: 4-wave (4, 16 spp) and 5-wave (64 spp)
+    builds, whole image and a slab split, against the oracle (rays and shadow rays counted once:
+    the second launch keeps counters of its own and adds only its sky and NaN pixels)."""
+    g = dt.globals_default()
+    built = dt.build_scene("spheres", 0, g)
+    g.perlin_cloud = 1
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = W, H, aa, depth
+    tile = dt.tiles(rank=world - 1, world=world, layout=dt.DT_OUT_SLAB) if world > 1 else dt.tiles()
+    gpu, ref, st, rst = _render_both(built, g, 0, tile)
+    assert rst.sky_pixels > 0 and st.sky_pixels > 0   # oracle: missed samples; GPU: pixels with one
+    _assert_same("spheres sky items %dx%d aa=%d world=%d" % (W, H, aa, world), gpu, ref, st, rst)
