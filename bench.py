@@ -201,11 +201,11 @@ def valu_roofline(cfg, kernel_ms, samples, ref_work=None, ref_samples=0, pmc=Non
 def trace_kernel_name(spp, models):
     """the trace kernel dt_render launches for the bench configs (frame 240, a still frame;
     dt_api.cpp enqueue_render): the 5-wave build at one pixel per wave, spp >= 64, unless DT_W5 says
-    otherwise; the room build without OBJ models, the *_full build with their triangles (C4)"""
+    otherwise; the room build without OBJ models, the *_mesh build with them (C4)"""
     e = os.environ.get("DT_W5")
     ppw = 64 // min(spp, 64)
     name = "dt_trace_kernel_w5" if ppw <= 8 and (e[:1] == "1" if e else spp >= 64) else "dt_trace_kernel"
-    return name + "_full" if models else name
+    return name + "_mesh" if models else name
 
 
 def load_pmc_traffic():

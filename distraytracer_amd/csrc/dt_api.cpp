@@ -30,12 +30,16 @@ extern "C" hipError_t dt_launch_normalize(const double* in, double* out, int64_t
   extern "C" const void* k##_ptr(void);                                                                \
   extern "C" int k##_traits(void);
 DT_TRACE_BUILD(dt_trace_kernel)
+DT_TRACE_BUILD(dt_trace_kernel_mesh)
 DT_TRACE_BUILD(dt_trace_kernel_full)
+DT_TRACE_BUILD(dt_trace_kernel_tunnel)
 DT_TRACE_BUILD(dt_trace_kernel_blur)
-DT_TRACE_BUILD(dt_trace_kernel_w5)
-DT_TRACE_BUILD(dt_trace_kernel_w5_full)
-DT_TRACE_BUILD(dt_trace_kernel_w5_blur)
 DT_TRACE_BUILD(dt_trace_kernel_sky)
+DT_TRACE_BUILD(dt_trace_kernel_w5)
+DT_TRACE_BUILD(dt_trace_kernel_w5_mesh)
+DT_TRACE_BUILD(dt_trace_kernel_w5_full)
+DT_TRACE_BUILD(dt_trace_kernel_w5_tunnel)
+DT_TRACE_BUILD(dt_trace_kernel_w5_blur)
 DT_TRACE_BUILD(dt_trace_kernel_w5_sky)
 DT_TRACE_BUILD(dt_trace_kernel_dn)
 DT_TRACE_BUILD(dt_trace_kernel_rpc)
@@ -154,7 +158,7 @@ struct dt_scene {
   float bump_pad = 0;          // y padding of its leaves: the largest |shift| a blur pass can draw
   bool bump_up_only = false;   // bump tree / blur-padded lists built for shifts >= 0 only
   bool no_cull = false;        // a RectPrismWithCylinder: no t-culling, no grid, no primary lists
-  bool room = false;           // every feature within DT_ROOM_FEATURES: the room builds can render it
+  unsigned features = ~0u;     // the scene's feature mask (dt_scene_dev.h): which builds can render it
   int kernel = DT_KERNEL_AUTO; // dt_scene_set_kernel
   ShadowGrid sg;
   void* d_sg_cells = nullptr;
@@ -313,11 +317,14 @@ int dt_scene_prepare(const dt_scene_desc* desc, const dt_globals* g, dt_scene** 
       if (desc->shapes[i].material == DT_MAT_GLASS) feat |= 1u << DT_FEAT_GLASS;
       if (desc->shapes[i].emit == DT_EMIT_SPHERE) feat |= 1u << DT_FEAT_SPHL;
     }
+    for (int i = 0; i < desc->n_shapes; ++i)
+      if (desc->shapes[i].emit == DT_EMIT_RECT) feat |= 1u << DT_FEAT_RECTL;
     for (int i = 0; i < desc->n_lights; ++i) {
       const int t = desc->lights[i].type;
-      if (t != DT_LIGHT_POINT && t != DT_LIGHT_RECT) feat |= 1u << DT_FEAT_SPHL;
+      if (t == DT_LIGHT_RECT) feat |= 1u << DT_FEAT_RECTL;
+      else if (t != DT_LIGHT_POINT) feat |= 1u << DT_FEAT_SPHL;
     }
-    s->room = (feat & ~DT_ROOM_FEATURES) == 0;
+    s->features = feat;
   }
   if (hipGetDevice(&s->device) != hipSuccess) {
     delete s;
@@ -726,14 +733,24 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
     int resident;
   };
 #define DT_B(k) {k##_launch, k##_ptr, k##_traits, 0}
-  static Build builds[10] = {DT_B(dt_trace_kernel),    DT_B(dt_trace_kernel_full),    DT_B(dt_trace_kernel_blur),
-                             DT_B(dt_trace_kernel_w5), DT_B(dt_trace_kernel_w5_full), DT_B(dt_trace_kernel_w5_blur),
-                             DT_B(dt_trace_kernel_dn), DT_B(dt_trace_kernel_rpc),   DT_B(dt_trace_kernel_sky),
-                             DT_B(dt_trace_kernel_w5_sky)};
+  // per wave count (4, 5): room, mesh, full (still frames); tunnel, blur (motion-blur frames); sky
+  static Build builds[2][6] = {
+      {DT_B(dt_trace_kernel), DT_B(dt_trace_kernel_mesh), DT_B(dt_trace_kernel_full),
+       DT_B(dt_trace_kernel_tunnel), DT_B(dt_trace_kernel_blur), DT_B(dt_trace_kernel_sky)},
+      {DT_B(dt_trace_kernel_w5), DT_B(dt_trace_kernel_w5_mesh), DT_B(dt_trace_kernel_w5_full),
+       DT_B(dt_trace_kernel_w5_tunnel), DT_B(dt_trace_kernel_w5_blur), DT_B(dt_trace_kernel_w5_sky)}};
+  static Build dn_build = DT_B(dt_trace_kernel_dn), rpc_build = DT_B(dt_trace_kernel_rpc);
 #undef DT_B
-  const int variant = blur ? 2 : sc->room ? 0 : 1;
-  Build& kb = sc->no_cull ? builds[7] : donate ? builds[6] : builds[(w5 ? 3 : 0) + variant];
-  Build& kb2 = builds[w5 ? 9 : 8];   // the *_sky build of the same wave count: renders the sky items
+  // DT_FULL_KERNEL=1: the builds with every feature for any scene (the tests' check of the
+  // feature builds against them)
+  const char* fk_env = getenv("DT_FULL_KERNEL");
+  const unsigned feats = fk_env && fk_env[0] == '1' ? ~0u : sc->features;
+  auto within = [&](unsigned mask) { return (feats & ~mask) == 0; };
+  const int variant = blur ? (within(DT_TUNNEL_FEATURES) ? 3 : 4)
+                           : within(DT_ROOM_FEATURES) ? 0 : within(DT_MESH_FEATURES) ? 1 : 2;
+  Build* const wb = builds[w5 ? 1 : 0];
+  Build& kb = sc->no_cull ? rpc_build : donate ? dn_build : wb[variant];
+  Build& kb2 = wb[5];   // the *_sky build of the same wave count: renders the sky items
   if (!kb.resident) kb.resident = max_resident_waves(kb.ptr(), 64);
   const int64_t waves = kb.resident;
   int64_t grid = P.n_items < waves ? P.n_items : waves;

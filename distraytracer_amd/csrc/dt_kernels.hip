@@ -109,40 +109,34 @@ using namespace dtd;
 #endif
 #define DT_AGAIN_QUEUE DT_SKY_BUILD
 // DT_FEATURES: the scene features a build handles (dt_scene_dev.h: bit t for shape type t,
-// DT_FEAT_SPHL sphere lights and emitters, DT_FEAT_ON Oren-Nayar, DT_FEAT_GLASS refraction). A build without some of them has
-// those cases compiled out; dt_api.cpp launches it only for scenes whose feature mask it covers.
+// DT_FEAT_SPHL sphere lights and emitters, DT_FEAT_RECTL rectangle lights and emitters, DT_FEAT_ON
+// Oren-Nayar, DT_FEAT_GLASS refraction). A build without some of them has those cases compiled out;
+// dt_api.cpp launches it only for scenes whose feature mask it covers.
 #ifndef DT_FEATURES
 #define DT_FEATURES 0xFFFFu
 #endif
 #define DT_HAS(bit) (((DT_FEATURES) >> (bit)) & 1u)
 #define DT_NEED(bit) do { if (!DT_HAS(bit)) __builtin_unreachable(); } while (0)
-#define DT_ROOM_BUILD ((DT_FEATURES) == DT_ROOM_FEATURES)
-// the trace-kernel builds (Makefile): work sharing, RectPrismWithCylinder, and the product kernels
-// at 5 and 4 waves per SIMD: still frames of room scenes (C2, C3, C5's room frames), still frames
-// of any scene (*_full: C4's meshes), frames with motion-blur shifts (*_blur)
-#if DT_WITH_RPC
+// DT_KNAME: the kernel's name, per build (Makefile TRACE_BUILDS: work sharing, RectPrismWithCylinder,
+// and the product kernels at 4 and 5 waves per SIMD for still frames of room scenes (C2, C3, C5's
+// room frames), of room scenes with meshes (*_mesh: C4), of any scene (*_full), for frames with
+// motion-blur shifts in tunnel scenes (*_tunnel) and in any scene (*_blur), and the *_sky builds
+// that render the items the still builds list)
+#ifdef DT_KNAME
+#define DT_TRACE_KERNEL DT_KNAME
+#elif DT_WITH_RPC
 #define DT_TRACE_KERNEL dt_trace_kernel_rpc
 #elif DT_DONATE
 #define DT_TRACE_KERNEL dt_trace_kernel_dn
-#elif DT_W5 && DT_SKY_BUILD
-#define DT_TRACE_KERNEL dt_trace_kernel_w5_sky
-#elif DT_SKY_BUILD
-#define DT_TRACE_KERNEL dt_trace_kernel_sky
-#elif DT_W5 && DT_NOSHIFT && DT_ROOM_BUILD
-#define DT_TRACE_KERNEL dt_trace_kernel_w5
-#elif DT_W5 && DT_NOSHIFT
-#define DT_TRACE_KERNEL dt_trace_kernel_w5_full
 #elif DT_W5
-#define DT_TRACE_KERNEL dt_trace_kernel_w5_blur
-#elif DT_NOSHIFT && DT_ROOM_BUILD
-#define DT_TRACE_KERNEL dt_trace_kernel
-#elif DT_NOSHIFT
-#define DT_TRACE_KERNEL dt_trace_kernel_full
+#define DT_TRACE_KERNEL dt_trace_kernel_w5
 #else
-#define DT_TRACE_KERNEL dt_trace_kernel_blur
+#define DT_TRACE_KERNEL dt_trace_kernel
 #endif
-// the 4-wave room build also carries the small kernels and the launch-record helpers
-#define DT_HELPERS (!DT_WITH_RPC && !DT_DONATE && !DT_ISECT && !DT_W5 && DT_NOSHIFT && DT_ROOM_BUILD)
+// DT_HELPERS=1 (the 4-wave room build): also the small kernels and the launch-record helpers
+#ifndef DT_HELPERS
+#define DT_HELPERS 0
+#endif
 
 #define DT_STACK_MAX 48
 #define DT_MAX_CLOUD_STEPS 2048
@@ -2043,6 +2037,7 @@ __device__ __forceinline__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L,
 {
   if (L.type == DT_LIGHT_POINT) return sub(v3a(L.center), point);
   if (L.type == DT_LIGHT_RECT) {
+    DT_NEED(DT_FEAT_RECTL);
     const bool odd = (li & 1) != 0;
     uint32_t w0, w1;
     if (odd && pair && pair[2] == (uint32_t)li) {
@@ -2599,7 +2594,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
           double f = (0.1 * pw1((double)hitdot) + 0.05 * pw5((double)hitdot)) + 0.9;
           own = mul(f, mul(k, shape_color));
         }
-        if (M.emit == DT_EMIT_RECT) {
+        if (DT_HAS(DT_FEAT_RECTL) && M.emit == DT_EMIT_RECT) {
           V3 A = G3(g, RC_A), B = G3(g, RC_B), C = G3(g, RC_C), D = G3(g, RC_D);
           float dist = (float)((((norm(sub(isectP, A)) + norm(sub(isectP, B))) + norm(sub(isectP, C))) +
                                 norm(sub(isectP, D))) /

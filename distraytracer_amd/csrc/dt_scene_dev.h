@@ -18,15 +18,20 @@
 #include <stdint.h>
 
 // Scene features a trace-kernel build handles (dt_kernels.hip DT_FEATURES; dt_api.cpp picks the
-// build from the scene's mask): bit t for shape type t (dt.h dt_shape_type), plus sphere lights
-// and "spherelight" emitters, Oren-Nayar materials and glass (refraction). The room build:
-// cylinders, rectangles, RectPrismV2, checkerboards with a hole, checker cylinders; point and
-// rectangle lights; Phong, Cook-Torrance and raw materials; no glass (buildFinal's room frames:
-// C2, C3, C5 n < 120).
+// build from the scene's mask): bit t for shape type t (dt.h dt_shape_type), sphere lights and
+// "spherelight" emitters, rectangle lights and "rectanglelight" emitters, Oren-Nayar materials and
+// glass (refraction). Point lights and Phong, Cook-Torrance and raw materials are in every build.
 #define DT_FEAT_SPHL 12
 #define DT_FEAT_ON 13
 #define DT_FEAT_GLASS 14
-#define DT_ROOM_FEATURES ((1u << 2) | (1u << 4) | (1u << 5) | (1u << 7) | (1u << 8))
+#define DT_FEAT_RECTL 15
+// buildFinal's room (C2, C3, C5 n < 120): cylinders, rectangles, RectPrismV2, checkerboards with a
+// hole, checker cylinders, rectangle lights
+#define DT_ROOM_FEATURES ((1u << 2) | (1u << 4) | (1u << 5) | (1u << 7) | (1u << 8) | (1u << DT_FEAT_RECTL))
+// the room with OBJ meshes (C4): + triangles, Oren-Nayar
+#define DT_MESH_FEATURES (DT_ROOM_FEATURES | (1u << 3) | (1u << DT_FEAT_ON))
+// buildFinal's tunnel (C5 n >= 140) and cloud frames: cylinders, triangles, rectangles, a point light
+#define DT_TUNNEL_FEATURES ((1u << 2) | (1u << 3) | (1u << 4))
 
 namespace dtd {
 

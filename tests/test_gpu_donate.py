@@ -123,3 +123,28 @@ def test_general_walks_match_product_walks(cuda, monkeypatch, case):
     gen, st1 = _render(g, built, frame, tile, False, monkeypatch)
     assert st0.rays == st1.rays and st0.shadow_rays == st1.shadow_rays
     log_equal("%s general walks vs product walks (bits)" % label, gen.view(np.uint32), base.view(np.uint32))
+
+
+FEATURE_CASES = [  # (id, builder args, frame, tile world): the build each scene's features select
+    ("c3_room_1of64_w5", ("final", 240, 0, 1920, 1080, 64, 8), 240, 64),
+    ("c2_room_full_w4", ("final", 240, 0, 800, 600, 16, 4), 240, 1),
+    ("c4_mesh_1of256_w5", ("final", 240, 1, 1920, 1080, 256, 8), 240, 256),
+    ("c5_tunnel_1920_1of512_w5", ("final", 1920, 0, 3840, 2160, 64, 10), 1920, 512),
+    ("c5_tunnel_1600_16spp_1of64_w4", ("final", 1600, 0, 960, 540, 16, 6), 1600, 64),
+]
+
+
+@pytest.mark.parametrize("case", FEATURE_CASES, ids=[c[0] for c in FEATURE_CASES])
+def test_feature_builds_match_full_builds(cuda, monkeypatch, case):
+    """Each scene takes the build whose features cover it (dt_api.cpp: room, mesh or full for still
+    frames; tunnel or blur for motion-blur frames); DT_FULL_KERNEL=1 renders it with the build that
+    has every feature. Same rays, same bits."""
+    label, args, frame, world = case
+    g, built = _globals(*args)
+    tile = dt.tiles(rank=0, world=world, layout=dt.DT_OUT_SLAB) if world > 1 else dt.tiles()
+    monkeypatch.setenv("DT_FULL_KERNEL", "0")
+    feat, st0 = _render(g, built, frame, tile, False, monkeypatch)
+    monkeypatch.setenv("DT_FULL_KERNEL", "1")
+    full, st1 = _render(g, built, frame, tile, False, monkeypatch)
+    assert st0.rays == st1.rays and st0.shadow_rays == st1.shadow_rays
+    log_equal("%s feature build vs full build (bits)" % label, feat.view(np.uint32), full.view(np.uint32))
