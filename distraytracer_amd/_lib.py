@@ -23,7 +23,7 @@ DT_KERNEL_AUTO, DT_KERNEL_PRODUCT, DT_KERNEL_DONATE = 0, 1, 2   # dt_scene_set_k
 
 SHAPE_TYPES = {1: "sphere", 2: "cylinder", 3: "triangle", 4: "rectangle", 5: "rectprism_v2",
                6: "checkerboard", 7: "checkerboard_hole", 8: "checker_cylinder", 9: "rectprism_cyl"}
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class ShapeDesc(ctypes.Structure):
@@ -104,7 +104,7 @@ class AccelInfo(ctypes.Structure):
                 ("sg_list_pool", c_int64), ("sg_list_entries", c_int64), ("nodes_hash", c_uint64),
                 ("fnodes_hash", c_uint64), ("bnodes_hash", c_uint64), ("sg_hash", c_uint64),
                 ("sg_contents_hash", c_uint64), ("bump_pad", c_float), ("sg_reach", c_float),
-                ("sg_umbra_cells", c_int64)]
+                ("sg_umbra_cells", c_int64), ("features", ctypes.c_uint32)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}

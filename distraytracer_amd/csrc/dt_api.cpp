@@ -286,6 +286,8 @@ static int scene_upload(dt_scene* s);
 // lists for the globals' camera. No device work, so it can run on a worker thread beside a render
 // that fills the GPU (the persistent trace kernel holds every CU, so even a copy's blit kernel
 // would wait for it: tools/animate.py builds frame n+1 this way and uploads it between frames).
+static unsigned scene_features(const dt_scene_desc& d);
+
 int dt_scene_prepare(const dt_scene_desc* desc, const dt_globals* g, dt_scene** out)
 {
   if (!desc || !g || !out) return fail(DT_E_INVALID, "null argument");
@@ -308,24 +310,7 @@ int dt_scene_prepare(const dt_scene_desc* desc, const dt_globals* g, dt_scene** 
     delete s;
     return fail(rc, err);
   }
-  {   // the scene's features (dt_scene_dev.h): whether the room builds of the trace kernel cover it
-    unsigned feat = 0;
-    for (int i = 0; i < desc->n_shapes; ++i) {
-      const int t = desc->shapes[i].type;
-      feat |= (t >= 0 && t < DT_FEAT_SPHL) ? 1u << t : 1u << 31;
-      if (desc->shapes[i].model == DT_MODEL_OREN_NAYAR) feat |= 1u << DT_FEAT_ON;
-      if (desc->shapes[i].material == DT_MAT_GLASS) feat |= 1u << DT_FEAT_GLASS;
-      if (desc->shapes[i].emit == DT_EMIT_SPHERE) feat |= 1u << DT_FEAT_SPHL;
-    }
-    for (int i = 0; i < desc->n_shapes; ++i)
-      if (desc->shapes[i].emit == DT_EMIT_RECT) feat |= 1u << DT_FEAT_RECTL;
-    for (int i = 0; i < desc->n_lights; ++i) {
-      const int t = desc->lights[i].type;
-      if (t == DT_LIGHT_RECT) feat |= 1u << DT_FEAT_RECTL;
-      else if (t != DT_LIGHT_POINT) feat |= 1u << DT_FEAT_SPHL;
-    }
-    s->features = feat;
-  }
+  s->features = scene_features(*desc);
   if (hipGetDevice(&s->device) != hipSuccess) {
     delete s;
     return fail(DT_E_NO_DEVICE, "no HIP device");
@@ -491,6 +476,26 @@ int dt_bvh_build(const dt_scene_desc* desc, const dt_globals* g, dt_bvh_node* no
   return export_bvh(b, nodes, cap, indices, index_cap, n_nodes, n_indices);
 }
 
+// the scene's features (dt_scene_dev.h): which trace-kernel builds can render it (enqueue_render)
+static unsigned scene_features(const dt_scene_desc& d)
+{
+  unsigned feat = 0;
+  for (int i = 0; i < d.n_shapes; ++i) {
+    const int t = d.shapes[i].type;
+    feat |= (t >= 0 && t < DT_FEAT_SPHL) ? 1u << t : 1u << 31;
+    if (d.shapes[i].model == DT_MODEL_OREN_NAYAR) feat |= 1u << DT_FEAT_ON;
+    if (d.shapes[i].material == DT_MAT_GLASS) feat |= 1u << DT_FEAT_GLASS;
+    if (d.shapes[i].emit == DT_EMIT_SPHERE) feat |= 1u << DT_FEAT_SPHL;
+    if (d.shapes[i].emit == DT_EMIT_RECT) feat |= 1u << DT_FEAT_RECTL;
+  }
+  for (int i = 0; i < d.n_lights; ++i) {
+    const int t = d.lights[i].type;
+    if (t == DT_LIGHT_RECT) feat |= 1u << DT_FEAT_RECTL;
+    else if (t != DT_LIGHT_POINT) feat |= 1u << DT_FEAT_SPHL;
+  }
+  return feat;
+}
+
 int dt_accel_info_build(const dt_scene_desc* desc, const dt_globals* g, dt_accel_info* info)
 {
   if (!desc || !g || !info) return fail(DT_E_INVALID, "null argument");
@@ -517,6 +522,7 @@ int dt_accel_info_build(const dt_scene_desc* desc, const dt_globals* g, dt_accel
   info->n_fnodes = a.n_fnodes;
   info->n_bnodes = a.n_bnodes;
   info->boxes_ordered = a.boxes_ordered;
+  info->features = scene_features(*desc);
   info->sg_lights = a.sg.n_lights;
   for (int k = 0; k < 3; ++k) info->sg_dim[k] = a.sg.dim[k];
   info->sg_cells = (int64_t)(a.sg.cells.size() / 2);
@@ -805,11 +811,11 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   const char* gw_env = getenv("DT_GENERAL_WALKS");
   if (gw_env && gw_env[0] == '1') PL.boxes_ordered = 0;
   // a still build without the sky march lists its items with a missed sample (multi-sample
-  // renders of a scene with perlin_cloud; dt_kernels.hip DT_SKY_AGAIN) and the *_sky build of the
-  // same wave count renders them in a second launch, with its own counters: the first launch
-  // already counted their rays and abort conditions, the second adds only their sky and NaN
-  // pixels (dt_collect_stats)
-  const bool again = (kb.traits() & 1) && PL.perlin_cloud && !PL.sky_defer;
+  // renders of a scene with perlin_cloud), the 5-wave one also those that needed an exact
+  // reference-tree walk (dt_kernels.hip DT_SKY_AGAIN, DT_GEN_AGAIN), and the *_sky build of the same
+  // wave count renders them in a second launch with counters of its own. Each listed item is
+  // counted by exactly one of the two launches; dt_collect_stats adds them up.
+  const bool again = (kb.traits() & 1) && ((kb.traits() & 2) || (PL.perlin_cloud && !PL.sky_defer));
   PL.sky_again = again ? 1 : 0;
   hs.again_list = nullptr;
   hs.again_n = nullptr;
@@ -858,7 +864,11 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   HIPCHK(kb.launch(sc->d_launch, out_dev, (int)grid, st));
   if (again) {
     if (!kb2.resident) kb2.resident = max_resident_waves(kb2.ptr(), 64);
-    HIPCHK(kb2.launch(sc->d_launch2, out_dev, (int)(grid < kb2.resident ? grid : kb2.resident), st));
+    // a few listed items in the scenes that use it (room frames: none to a handful): 512 waves
+    // start and drain faster than a full persistent grid
+    int64_t g2 = grid < kb2.resident ? grid : kb2.resident;
+    g2 = g2 < 512 ? g2 : 512;
+    HIPCHK(kb2.launch(sc->d_launch2, out_dev, (int)g2, st));
   }
   sc->again_used = again;
   if (PL.sky_defer) HIPCHK(dt_launch_sky_miss(sc->d_launch, out_dev, n_px, st));
@@ -879,11 +889,10 @@ int dt_collect_stats(const dt_scene* sc_c, void* stream, dt_stats* stats)
   if (!stats) return DT_OK;
   unsigned long long h[ST_N];
   HIPCHK(hipMemcpy(h, sc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
-  if (sc->again_used) {   // the sky items' second launch: their sky and NaN pixels
+  if (sc->again_used) {   // the listed items' second launch (dt_kernels.hip DT_SKY_AGAIN)
     unsigned long long h2[ST_N];
     HIPCHK(hipMemcpy(h2, sc->d_stats2, sizeof(h2), hipMemcpyDeviceToHost));
-    h[ST_SKY] += h2[ST_SKY];
-    h[ST_NAN] += h2[ST_NAN];
+    for (int k = 0; k < ST_N; ++k) h[k] += h2[k];
   }
   memset(stats, 0, sizeof(*stats));
   const dtd::DParams& P = sc->last;

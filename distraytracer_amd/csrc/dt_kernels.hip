@@ -108,6 +108,13 @@ using namespace dtd;
 #define DT_SKY_AGAIN 0
 #endif
 #define DT_AGAIN_QUEUE DT_SKY_BUILD
+// DT_GEN_AGAIN (the 5-wave still builds): the exact reference-tree walks of waves with an
+// axis-parallel or NaN ray (and the edge-on checkerboard repeat) are not compiled in either. Such a
+// wave takes the item back (its counters restored) and lists it, flagged, for the *_sky build,
+// which renders and counts it (SGPR spills 138 -> 77, C3 +2%; profiles/r04z_ab_gen_again.log).
+#ifndef DT_GEN_AGAIN
+#define DT_GEN_AGAIN (DT_SKY_AGAIN && DT_W5)
+#endif
 // DT_FEATURES: the scene features a build handles (dt_scene_dev.h: bit t for shape type t,
 // DT_FEAT_SPHL sphere lights and emitters, DT_FEAT_RECTL rectangle lights and emitters, DT_FEAT_ON
 // Oren-Nayar, DT_FEAT_GLASS refraction). A build without some of them has those cases compiled out;
@@ -997,7 +1004,7 @@ __device__ bool shape_shadow(int type, uint32_t flags, GP g, V3 ray, V3 start,
 // GeoPrimitive::getNorm (per-lane shape index); ccol: the hit record's colour offset (a
 // RectPrismWithCylinder hole: its record is at ccol - RH_COL)
 __device__ __forceinline__ V3 shape_norm(int type, uint32_t flags, GP g, V3 p, float shift,
-                         unsigned long long* st_prism, int ccol)
+                         unsigned int* st_prism, int ccol)
 {
   switch (type) {
 #if DT_WITH_RPC
@@ -1011,7 +1018,7 @@ __device__ __forceinline__ V3 shape_norm(int type, uint32_t flags, GP g, V3 p, f
       if (dot(pa, G3(g, RP_NFRONT)) <= eps) return G3(g, RP_NFRONT);
       // the reference throws ("point is not on prism", 1819-1820): counted; the hit hole's normal
       // (Cylinder::getNorm, 419-425), else the front normal
-      atomicAdd(st_prism, 1ull);
+      atomicAdd(st_prism, 1u);
       if (ccol >= 0) {
         const int h = ccol - RH_COL;
         const V3 axis = G3(g, h + RH_AX), pc = sub(p, G3(g, h + RH_C1));
@@ -1054,7 +1061,7 @@ __device__ __forceinline__ V3 shape_norm(int type, uint32_t flags, GP g, V3 p, f
       if (pa_right <= eps || pg_right <= eps) return nr;
       float pa_front = (float)fabs(dot(pa, nf)), pg_front = (float)fabs(dot(pg, nf));
       if (pa_front <= eps || pg_front <= eps) return nf;
-      atomicAdd(st_prism, 1ull);
+      atomicAdd(st_prism, 1u);
       float m = pa_bot;
       if (pg_bot < m) m = pg_bot;
       if (pa_right < m) m = pa_right;
@@ -1546,6 +1553,9 @@ __device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams
 // address of the caller's hit record or counters escapes into memory.
 // Out of line in the 4-wave still builds only: C2 +5%, but the 5-wave build (96 VGPRs) loses 7.5% on
 // C3 to the call's register save/restore (profiles/r04r_ab_general_ool.log)
+#if DT_GEN_AGAIN
+__shared__ int dt_gen_again;   // the wave's item needs an exact reference-tree walk
+#endif
 #ifndef DT_GENERAL_OOL
 #define DT_GENERAL_OOL (DT_NOSHIFT && !DT_W5)
 #endif
@@ -1593,8 +1603,14 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
                                             HitRec& h, CNT& cnt, int pblock = -1)
 {
   const Walk w = make_walk(P, active, ray, org, shift);
-  if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift)))
+  if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift))) {
+#if DT_GEN_AGAIN
+    dt_gen_again = 1;   // the item goes to the *_sky build
+    return false;
+#else
     return closest_hit_exact(S, P, w, active, ray, org, shift, h, cnt);
+#endif
+  }
   bool any;
   if (pblock >= 0 && (!w.bump_wave || P.pl_bump)) {
     // blur passes take the bump tree's lists, stored after the pass-0 lists
@@ -1609,8 +1625,14 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
   // an edge-on checkerboard hit keeps the previous test's t (Q16): only the reference order
   // reproduces it, so with the alternative trees such waves (never seen in practice) repeat the
   // walk on the reference tree
-  if ((w.bump_wave || (P.n_fnodes > 0 && (P.ftree_mode & 1))) && __ballot(h.edge))
+  if ((w.bump_wave || (P.n_fnodes > 0 && (P.ftree_mode & 1))) && __ballot(h.edge)) {
+#if DT_GEN_AGAIN
+    dt_gen_again = 1;
+    return any;
+#else
     return closest_hit_exact(S, P, w, active, ray, org, shift, h, cnt);
+#endif
+  }
   return any;
 }
 
@@ -1825,7 +1847,10 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   cnt.cur_path = 2;
 #endif
   if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift))) {
-#if DT_GENERAL_OOL
+#if DT_GEN_AGAIN
+    dt_gen_again = 1;
+    return false;
+#elif DT_GENERAL_OOL
     const GeneralOcc<CNT> o = occluded_general(&S, &P, w, active, bstart, sn, sstart, t_max, skip_shape, cnt);
     cnt = o.cnt;
     return o.occl;
@@ -1938,7 +1963,11 @@ struct PassOut {
 // wave-level event counters of dt_stats (rays, shadow rays, texel fetches) in the wave's LDS: one
 // lane adds the ballot's popcount. Per-lane counters in VGPRs were live across every walk and
 // spilled/reloaded around them (a scratch store per light iteration).
-enum { WC_RAYS = 0, WC_SHADOW = 1, WC_TEX = 2, WC_N = 3 };
+// The abort conditions the reference reports (stack overflows, reflection errors, glossy and
+// sphere-light resample exhaustion, UV out of range, prism-normal fallbacks) count per lane into the
+// same LDS words (LDS atomics), so that an item's counts can be taken back (DT_SKY_AGAIN items).
+enum { WC_RAYS = 0, WC_SHADOW = 1, WC_TEX = 2, WC_STACK = 3, WC_REFL = 4, WC_GLOSSY = 5, WC_UV = 6, WC_PRISM = 7,
+       WC_SPHL = 8, WC_N = 9 };
 #define DT_WCNT(k, cond)                                                                 \
   do {                                                                                   \
     const unsigned long long m_ = __ballot(cond);                                        \
@@ -2000,7 +2029,7 @@ __device__ __forceinline__ V3 rect_sample(V3 A, V3 B, V3 D, double u0, double u1
 // sampling with acos/sin/cos (no C2-C5 scene has a sphere light). Everything stays inlined: a real
 // call anywhere in the trace kernel costs ~25% (calling-convention register saves/spills)
 __device__ __forceinline__ V3 sphere_light_sample(const Ctx& c, const DT_CAS DLight& L, int li, V3 point,
-                                                            uint32_t node, unsigned long long* st_sphl)
+                                                            uint32_t node, unsigned int* st_sphl)
 {
   V3 C = v3a(L.center), baxis = v3a(L.baxis);
   int attempt = 0;
@@ -2011,7 +2040,7 @@ __device__ __forceinline__ V3 sphere_light_sample(const Ctx& c, const DT_CAS DLi
   V3 tmp = add(mul(L.radius, dir), C);
   int sample_limit = 20;
   while (dot(sub(tmp, C), sub(point, C)) < 0 || (L.use_baxis && dot(sub(tmp, C), baxis) < 0)) {
-    if (sample_limit < 0) { if (st_sphl) atomicAdd(st_sphl, 1ull); break; }
+    if (sample_limit < 0) { if (st_sphl) atomicAdd(st_sphl, 1u); break; }
     V3 rev = add(mul(-L.radius, dir), C);
     if (dot(sub(rev, C), sub(point, C)) >= 0 && (!L.use_baxis || dot(sub(rev, C), baxis) >= 0)) {
       tmp = rev;
@@ -2033,7 +2062,7 @@ __device__ __forceinline__ V3 sphere_light_sample(const Ctx& c, const DT_CAS DLi
 // 2-3 light 2k+1's. `pair` keeps words 2-3 of an even light's draw, with
 // pair[2] = the odd light they belong to, so the odd light does not draw again.
 __device__ __forceinline__ V3 light_sample(const Ctx& c, const DT_CAS DLight& L, int li, V3 point, uint32_t node,
-                                           unsigned long long* st_sphl, uint32_t* pair = nullptr)
+                                           unsigned int* st_sphl, uint32_t* pair = nullptr)
 {
   if (L.type == DT_LIGHT_POINT) return sub(v3a(L.center), point);
   if (L.type == DT_LIGHT_RECT) {
@@ -2334,7 +2363,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
               stack[sp].key = r.aux;
               ++sp;
             } else {
-              atomicAdd(S.stats + ST_STACK, 1ull);
+              atomicAdd(cnt.wc + WC_STACK, 1u);
             }
             break;
           } else {   // DN_END: the list's (largest pre-order path, in_motion)
@@ -2446,7 +2475,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
       GP g = cas(S.geom) + hd.off;
       const DMat& M = S.mat[sid];
       isectP = add(eye, mul(h.t_min, ray));
-      normal = shape_norm(hd.type, hd.flags, g, isectP, shift, S.stats + ST_PRISM, h.ccol);
+      normal = shape_norm(hd.type, hd.flags, g, isectP, shift, cnt.wc + WC_PRISM, h.ccol);
       in = normalized(ray);
       shape_color = h.ccol >= 0 ? G3(g, h.ccol) : v3a(M.color);
 #if DT_DONATE
@@ -2463,7 +2492,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
 
       // reserve the FINISH slot below the children
       if (sp < DT_STACK_MAX) { fin_slot = sp++; }
-      else atomicAdd(S.stats + ST_STACK, 1ull);
+      else atomicAdd(cnt.wc + WC_STACK, 1u);
 
       if (P.reflect && is_refl_material(M.material)) {
         const float eps = 1e-3f;
@@ -2490,12 +2519,12 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
           V3 refl_ray = sub(in, mul(2 * dot(normal, in), normal));
           const double rn = dot(refl_ray, normal);
           int nref = 0;
-          if (rn <= 0) atomicAdd(S.stats + ST_REFL, 1ull);
+          if (rn <= 0) atomicAdd(cnt.wc + WC_REFL, 1u);
           else if (rn > eps) nref = (glossy && !P.nogloss) ? P.brdf_samples : 1;
           const bool glass = DT_HAS(DT_FEAT_GLASS) && M.material == DT_MAT_GLASS;
           const int base = sp;
           if (base + nref + (glass ? 1 : 0) > DT_STACK_MAX) {
-            atomicAdd(S.stats + ST_STACK, 1ull);
+            atomicAdd(cnt.wc + WC_STACK, 1u);
             nref = 0;
           } else {
             sp = base + nref;
@@ -2568,7 +2597,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
                   sample_refl = sub(rect_sample_f(A, B, D, gx, gy), isectP);
                   sample_limit--;
                 }
-                if (exhausted) atomicAdd(S.stats + ST_GLOSSY, 1ull);
+                if (exhausted) atomicAdd(cnt.wc + WC_GLOSSY, 1u);
                 Entry ch; ch.a = sample_refl; ch.b = add(isectP, mul(eps, sample_refl));
                 ch.k = kg; ch.depth = exhausted ? 0 : depth - 1; ch.key = child_key(node, 2 + i);
                 ch._pad = DT_CPATH(2 + i);
@@ -2665,7 +2694,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
         V3 sn = v3(1, 0, 0);
         if (walk) {
           DT_WK(DT_WK_LIGHT, true);
-          sray = light_sample(c, L, li, isectP, node, S.stats + ST_SPHL, pair);
+          sray = light_sample(c, L, li, isectP, node, cnt.wc + WC_SPHL, pair);
           t_max = (float)norm(sray);
           sn = normalized(sray);
           DT_WCNT(WC_SHADOW, true);
@@ -2702,7 +2731,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
           if (textured) {
             DT_WK(DT_WK_TEX, !tex_counted);   // getUV + texel once per node, as the two-pass count
             DT_WORK(tex_counted = true);
-            if (uv_oob) atomicAdd(S.stats + ST_UV, 1ull);   // the reference terminates here (Q9)
+            if (uv_oob) atomicAdd(cnt.wc + WC_UV, 1u);   // the reference terminates here (Q9)
             DT_WCNT(WC_TEX, uvt == 1 && M.tex >= 0);
           }
           const V3 ray_col = brdf(P, M, cas(S.lights)[li], normal, e_dir, sray, sn, shape_color);
@@ -2898,6 +2927,9 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   unsigned long long sky_px = 0;
   Counters cnt;
   __shared__ unsigned int wc_lds[WC_N];
+#if DT_SKY_AGAIN || DT_AGAIN_QUEUE
+  __shared__ unsigned int wc_snap[WC_N];
+#endif
   if (lane < WC_N) wc_lds[lane] = 0;
   __syncthreads();
   cnt.wc = wc_lds;
@@ -2938,8 +2970,18 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       __syncthreads();
     }
     if (qpos >= n_queue) break;
-    const int64_t item = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)S.again_list[qpos] : qpos;
+    const uint32_t entry = DT_AGAIN_QUEUE && P.sky_again == 2 ? S.again_list[qpos] : 0u;
+    const int64_t item = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)(entry & 0x7fffffffu) : qpos;
     bool sky_again = false;
+#if DT_SKY_AGAIN || DT_AGAIN_QUEUE
+    // the item's counters can be taken back: a listed item is counted by exactly one launch
+    if (lane < WC_N) wc_snap[lane] = wc_lds[lane];
+    const uint32_t wnodes0 = cnt.wnodes;
+#endif
+#if DT_GEN_AGAIN
+    if (lane == 0) dt_gen_again = 0;
+    __syncthreads();
+#endif
 
     const int group = P.ppw;
     const int spp = P.spp;
@@ -3074,12 +3116,19 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       __syncthreads();
     }
     DT_T(k3);
+#if DT_GEN_AGAIN
+    __syncthreads();
+    const bool gen_again = __builtin_amdgcn_readfirstlane(dt_gen_again) != 0;
+#else
+    const bool gen_again = false;
+#endif
+    const bool item_again = sky_again || gen_again;
     if (lane < group) {
       int qx, qy;
       int64_t qo;
       bool qv;
       pixel_of(P, item * group + lane, qx, qy, qo, qv);
-      if (qv && !sky_again && !(P.sky_defer && S.sky_miss[item * group + lane])) {
+      if (qv && !item_again && !(P.sky_defer && S.sky_miss[item * group + lane])) {
         V3 color = divs(v3(psum[0][lane], psum[1][lane], psum[2][lane]), spp);
 #ifdef DT_ITEM_TIMES   // diagnostic builds (tools/item_times.py): the item's wave cycles / 1e4, raw
         {
@@ -3093,7 +3142,18 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
       }
     }
-    if (sky_again && lane == 0) S.again_list[atomicAdd(S.again_n, 1u)] = (uint32_t)item;
+#if DT_SKY_AGAIN || DT_AGAIN_QUEUE
+    // items left to the *_sky build: a sky item is counted here, an item that needed an exact walk
+    // (flag bit 31) there; the *_sky build takes back the counts of the sky items it renders
+    if (gen_again || (DT_AGAIN_QUEUE && P.sky_again == 2 && !(entry >> 31))) {
+      __syncthreads();
+      if (lane < WC_N) wc_lds[lane] = wc_snap[lane];
+      cnt.wnodes = wnodes0;
+      __syncthreads();
+    }
+    if (item_again && lane == 0)
+      S.again_list[atomicAdd(S.again_n, 1u)] = (uint32_t)item | (gen_again ? 0x80000000u : 0u);
+#endif
     if (P.prio_steps > 0) __builtin_amdgcn_s_setprio(0);
     ++qpos;
   }
@@ -3119,6 +3179,9 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       atomicAdd(S.stats + ST_RAYS, r);
       atomicAdd(S.stats + ST_SHADOW, sh);
       atomicAdd(S.stats + ST_TEX, tx);
+      const int st_of[WC_N] = {-1, -1, -1, ST_STACK, ST_REFL, ST_GLOSSY, ST_UV, ST_PRISM, ST_SPHL};
+      for (int k = WC_STACK; k < WC_N; ++k)
+        if (wc_lds[k]) atomicAdd(S.stats + st_of[k], (unsigned long long)wc_lds[k]);
     }
   }
 }
@@ -3276,6 +3339,7 @@ extern "C" hipError_t DT_CAT(DT_TRACE_KERNEL, _launch)(const void* dev_launch, f
   return hipGetLastError();
 }
 extern "C" const void* DT_CAT(DT_TRACE_KERNEL, _ptr)(void) { return (const void*)DT_TRACE_KERNEL; }
-// bit 0: the build lists sky items for another launch (DT_SKY_AGAIN)
-extern "C" int DT_CAT(DT_TRACE_KERNEL, _traits)(void) { return DT_SKY_AGAIN ? 1 : 0; }
+// bit 0: the build lists sky items for another launch (DT_SKY_AGAIN); bit 1: also the items that
+// needed an exact reference-tree walk (DT_GEN_AGAIN)
+extern "C" int DT_CAT(DT_TRACE_KERNEL, _traits)(void) { return (DT_SKY_AGAIN ? 1 : 0) | (DT_GEN_AGAIN ? 2 : 0); }
 #endif

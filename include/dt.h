@@ -41,7 +41,8 @@ extern "C" {
  *    (DT_SHAPE_RECTPRISM_CYL with the dt_scene_desc.holes array) */
 /* 3: dt_stats.donations / donate_overflow (DFS work sharing inside a wave, DT_DONATE) */
 /* 4: dt_scene_set_kernel (the trace-kernel choice per scene, not through the environment) */
-#define DT_ABI_VERSION 4
+/* 5: dt_accel_info.features */
+#define DT_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------- */
 #define DT_OK              0
@@ -304,6 +305,9 @@ typedef struct dt_accel_info {
   uint64_t sg_contents_hash;   /* each cell's list as a sorted set (order-free) */
   float bump_pad, sg_reach;
   int64_t sg_umbra_cells;      /* (light, cell) records whose every segment to the light is occluded */
+  uint32_t features;           /* the scene's trace-kernel feature mask: bit t for shape type t,
+                                  12 sphere lights/emitters, 13 Oren-Nayar, 14 glass, 15 rectangle
+                                  lights/emitters (the build dt_render launches) */
 } dt_accel_info;
 int dt_accel_info_build(const dt_scene_desc* desc, const dt_globals* g, dt_accel_info* info);
 

@@ -386,3 +386,30 @@ def test_oracle_primary_hit_numbering():
     s2, t2 = oracle.primary_hit(b, g, 240, 100, 256, nthreads=1)
     s3, t3 = oracle.primary_hit(b, g, 240, 356, 256, nthreads=2)
     assert np.array_equal(s1, np.concatenate([s2, s3])) and np.array_equal(t1, np.concatenate([t2, t3]))
+
+
+# the trace-kernel feature masks (distraytracer_amd/csrc/dt_scene_dev.h)
+_ROOM = (1 << 2) | (1 << 4) | (1 << 5) | (1 << 7) | (1 << 8) | (1 << 15)
+_MESH = _ROOM | (1 << 3) | (1 << 13)
+_TUNNEL = (1 << 2) | (1 << 3) | (1 << 4)
+
+
+@pytest.mark.parametrize("name,frame,models,build", [
+    ("final", 240, 0, "room"), ("final", 0, 0, "room"), ("final", 952, 0, "room"),
+    ("final", 240, 1, "mesh"), ("final", 1120, 0, "tunnel"), ("final", 1920, 0, "tunnel"),
+    ("final", 2000, 0, "tunnel"), ("spheres", 0, 0, "full"), ("prismcyl", 7, 0, "full")])
+def test_scene_features_select_the_build(name, frame, models, build):
+    """dt_accel_info.features: the scene's feature mask, from which dt_render picks the trace-kernel
+    build (room / mesh / full for still frames, tunnel / full blur for motion-blur frames). The C2,
+    C3 and C5 room frames take the room build, C4 the mesh build, C5's tunnel and cloud frames the
+    tunnel build; the spheres scene (spheres, sphere lights) and RectPrismWithCylinder the full."""
+    g = dt.globals_default()
+    g.use_model = models
+    built = dt.build_scene(name, frame, g)
+    f = dt.accel_info(built, g)["features"]
+    within = lambda m: f & ~m == 0
+    if frame >= g.frame_prism:   # motion-blur frames (dt_api.cpp enqueue_render)
+        got = "tunnel" if within(_TUNNEL) else "full"
+    else:
+        got = "room" if within(_ROOM) else "mesh" if within(_MESH) else "full"
+    assert got == build, "features %#x" % f
