@@ -811,11 +811,11 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   const char* gw_env = getenv("DT_GENERAL_WALKS");
   if (gw_env && gw_env[0] == '1') PL.boxes_ordered = 0;
   // a still build without the sky march lists its items with a missed sample (multi-sample
-  // renders of a scene with perlin_cloud), the 5-wave one also those that needed an exact
-  // reference-tree walk (dt_kernels.hip DT_SKY_AGAIN, DT_GEN_AGAIN), and the *_sky build of the same
-  // wave count renders them in a second launch with counters of its own. Each listed item is
-  // counted by exactly one of the two launches; dt_collect_stats adds them up.
-  const bool again = (kb.traits() & 1) && ((kb.traits() & 2) || (PL.perlin_cloud && !PL.sky_defer));
+  // renders of a scene with perlin_cloud; dt_kernels.hip DT_SKY_AGAIN) and the *_sky build of the
+  // same wave count renders them in a second launch with counters of its own. The first launch
+  // counts the listed items, the second takes their counts back but for their sky and NaN pixels;
+  // dt_collect_stats adds the two up.
+  const bool again = (kb.traits() & 1) && PL.perlin_cloud && !PL.sky_defer;
   PL.sky_again = again ? 1 : 0;
   hs.again_list = nullptr;
   hs.again_n = nullptr;

@@ -108,13 +108,6 @@ using namespace dtd;
 #define DT_SKY_AGAIN 0
 #endif
 #define DT_AGAIN_QUEUE DT_SKY_BUILD
-// DT_GEN_AGAIN (the 5-wave still builds): the exact reference-tree walks of waves with an
-// axis-parallel or NaN ray (and the edge-on checkerboard repeat) are not compiled in either. Such a
-// wave takes the item back (its counters restored) and lists it, flagged, for the *_sky build,
-// which renders and counts it (SGPR spills 138 -> 77, C3 +2%; profiles/r04z_ab_gen_again.log).
-#ifndef DT_GEN_AGAIN
-#define DT_GEN_AGAIN (DT_SKY_AGAIN && DT_W5)
-#endif
 // DT_FEATURES: the scene features a build handles (dt_scene_dev.h: bit t for shape type t,
 // DT_FEAT_SPHL sphere lights and emitters, DT_FEAT_RECTL rectangle lights and emitters, DT_FEAT_ON
 // Oren-Nayar, DT_FEAT_GLASS refraction). A build without some of them has those cases compiled out;
@@ -1553,9 +1546,6 @@ __device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams
 // address of the caller's hit record or counters escapes into memory.
 // Out of line in the 4-wave still builds only: C2 +5%, but the 5-wave build (96 VGPRs) loses 7.5% on
 // C3 to the call's register save/restore (profiles/r04r_ab_general_ool.log)
-#if DT_GEN_AGAIN
-__shared__ int dt_gen_again;   // the wave's item needs an exact reference-tree walk
-#endif
 #ifndef DT_GENERAL_OOL
 #define DT_GENERAL_OOL (DT_NOSHIFT && !DT_W5)
 #endif
@@ -1604,12 +1594,7 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
 {
   const Walk w = make_walk(P, active, ray, org, shift);
   if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift))) {
-#if DT_GEN_AGAIN
-    dt_gen_again = 1;   // the item goes to the *_sky build
-    return false;
-#else
     return closest_hit_exact(S, P, w, active, ray, org, shift, h, cnt);
-#endif
   }
   bool any;
   if (pblock >= 0 && (!w.bump_wave || P.pl_bump)) {
@@ -1626,12 +1611,7 @@ __device__ __forceinline__ bool closest_hit(const DScene& S, const DParams& P, b
   // reproduces it, so with the alternative trees such waves (never seen in practice) repeat the
   // walk on the reference tree
   if ((w.bump_wave || (P.n_fnodes > 0 && (P.ftree_mode & 1))) && __ballot(h.edge)) {
-#if DT_GEN_AGAIN
-    dt_gen_again = 1;
-    return any;
-#else
     return closest_hit_exact(S, P, w, active, ray, org, shift, h, cnt);
-#endif
   }
   return any;
 }
@@ -1847,10 +1827,7 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
   cnt.cur_path = 2;
 #endif
   if (w.inf_wave || (w.bump_wave && !bump_tree_ok(P, active, shift))) {
-#if DT_GEN_AGAIN
-    dt_gen_again = 1;
-    return false;
-#elif DT_GENERAL_OOL
+#if DT_GENERAL_OOL
     const GeneralOcc<CNT> o = occluded_general(&S, &P, w, active, bstart, sn, sstart, t_max, skip_shape, cnt);
     cnt = o.cnt;
     return o.occl;
@@ -2927,7 +2904,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   unsigned long long sky_px = 0;
   Counters cnt;
   __shared__ unsigned int wc_lds[WC_N];
-#if DT_SKY_AGAIN || DT_AGAIN_QUEUE
+#if DT_AGAIN_QUEUE
   __shared__ unsigned int wc_snap[WC_N];
 #endif
   if (lane < WC_N) wc_lds[lane] = 0;
@@ -2970,17 +2947,12 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       __syncthreads();
     }
     if (qpos >= n_queue) break;
-    const uint32_t entry = DT_AGAIN_QUEUE && P.sky_again == 2 ? S.again_list[qpos] : 0u;
-    const int64_t item = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)(entry & 0x7fffffffu) : qpos;
+    const int64_t item = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)S.again_list[qpos] : qpos;
     bool sky_again = false;
-#if DT_SKY_AGAIN || DT_AGAIN_QUEUE
-    // the item's counters can be taken back: a listed item is counted by exactly one launch
+#if DT_AGAIN_QUEUE
+    // the item's counters are taken back: the launch that listed it counted it already
     if (lane < WC_N) wc_snap[lane] = wc_lds[lane];
     const uint32_t wnodes0 = cnt.wnodes;
-#endif
-#if DT_GEN_AGAIN
-    if (lane == 0) dt_gen_again = 0;
-    __syncthreads();
 #endif
 
     const int group = P.ppw;
@@ -3116,13 +3088,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       __syncthreads();
     }
     DT_T(k3);
-#if DT_GEN_AGAIN
-    __syncthreads();
-    const bool gen_again = __builtin_amdgcn_readfirstlane(dt_gen_again) != 0;
-#else
-    const bool gen_again = false;
-#endif
-    const bool item_again = sky_again || gen_again;
+    const bool item_again = sky_again;
     if (lane < group) {
       int qx, qy;
       int64_t qo;
@@ -3142,17 +3108,18 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
       }
     }
-#if DT_SKY_AGAIN || DT_AGAIN_QUEUE
-    // items left to the *_sky build: a sky item is counted here, an item that needed an exact walk
-    // (flag bit 31) there; the *_sky build takes back the counts of the sky items it renders
-    if (gen_again || (DT_AGAIN_QUEUE && P.sky_again == 2 && !(entry >> 31))) {
+#if DT_AGAIN_QUEUE
+    // a listed item is counted by the launch that listed it: the *_sky build takes its counts back
+    // (all but its sky and NaN pixels, which only this launch stores)
+    if (P.sky_again == 2) {
       __syncthreads();
       if (lane < WC_N) wc_lds[lane] = wc_snap[lane];
       cnt.wnodes = wnodes0;
       __syncthreads();
     }
-    if (item_again && lane == 0)
-      S.again_list[atomicAdd(S.again_n, 1u)] = (uint32_t)item | (gen_again ? 0x80000000u : 0u);
+#endif
+#if DT_SKY_AGAIN
+    if (item_again && lane == 0) S.again_list[atomicAdd(S.again_n, 1u)] = (uint32_t)item;
 #endif
     if (P.prio_steps > 0) __builtin_amdgcn_s_setprio(0);
     ++qpos;
@@ -3339,7 +3306,6 @@ extern "C" hipError_t DT_CAT(DT_TRACE_KERNEL, _launch)(const void* dev_launch, f
   return hipGetLastError();
 }
 extern "C" const void* DT_CAT(DT_TRACE_KERNEL, _ptr)(void) { return (const void*)DT_TRACE_KERNEL; }
-// bit 0: the build lists sky items for another launch (DT_SKY_AGAIN); bit 1: also the items that
-// needed an exact reference-tree walk (DT_GEN_AGAIN)
-extern "C" int DT_CAT(DT_TRACE_KERNEL, _traits)(void) { return (DT_SKY_AGAIN ? 1 : 0) | (DT_GEN_AGAIN ? 2 : 0); }
+// bit 0: the build lists sky items for another launch (DT_SKY_AGAIN)
+extern "C" int DT_CAT(DT_TRACE_KERNEL, _traits)(void) { return DT_SKY_AGAIN ? 1 : 0; }
 #endif

@@ -19,11 +19,11 @@ def main(tag, kernel="dt_trace_kernel", config="c3"):
     for f in glob.glob(os.path.join(src, "*", "*_counter_collection.csv")):
         seen = set()
         for r in csv.DictReader(open(f)):
-            if kernel not in r["Kernel_Name"]:
+            if r["Kernel_Name"].split("(")[0] != kernel:   # exact: not dt_trace_kernel_w5_sky
                 continue
             acc[r["Counter_Name"]] += float(r["Counter_Value"])
             seen.add(r["Dispatch_Id"])
-        for c in {r["Counter_Name"] for r in csv.DictReader(open(f)) if kernel in r["Kernel_Name"]}:
+        for c in {r["Counter_Name"] for r in csv.DictReader(open(f)) if r["Kernel_Name"].split("(")[0] == kernel}:
             n_disp[c] = len(seen)
     per = {k: v / max(n_disp[k], 1) for k, v in acc.items()}
     stats = os.path.join(src, "kt", "kt_kernel_stats.csv")
