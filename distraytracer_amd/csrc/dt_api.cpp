@@ -782,7 +782,10 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   const char* bi = getenv("DT_BATCH_ITEMS");
   const char* bs = getenv("DT_BATCH_SIZE");
   const int64_t batch_from = bi && atoi(bi) > 0 ? atoi(bi) : 32;
-  PL.item_batch = PL.n_items >= batch_from * grid ? (bs && atoi(bs) > 0 ? atoi(bs) : 2) : 1;
+  // Items of several 64-sample chunks (spp > 64: C4's 256) take one per atomic: their dequeues are
+  // rare already, and two consecutive pixels per wave cost C4 2.7% (profiles/r04zl_c4_batch.log)
+  PL.item_batch = PL.n_items >= batch_from * grid && (PL.chunks == 1 || (bs && atoi(bs) > 0))
+                      ? (bs && atoi(bs) > 0 ? atoi(bs) : 2) : 1;
   // deep-cascade waves raise their priority (dt_kernels.hip, DT_PRIO_STEPS) when the frame is split
   // over ranks, where one such wave bounds a rank's kernel; DT_PRIO_STEPS=<n> overrides (0: off)
   const char* ps = getenv("DT_PRIO_STEPS");
