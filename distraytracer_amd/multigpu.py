@@ -1,12 +1,15 @@
 """Image-space tile split across ranks + gather of finished tiles.
 
-Every rank holds the whole (tiny) scene and renders one 8x8 tile of every group of `world`
+Every rank holds the whole (tiny) scene and renders one tile of every group of `world`
 consecutive tiles (raster order), the ranks rotated by a hash of the group (dt_scene_dev.h
 tile_of), into a packed slab: the expensive sky/glossy regions spread over all GPUs, and unlike a
-plain t % world interleave no rank is tied to a fixed set of tile columns. 8x8 (the primary
-lists' block) rather than the ABI's default 32x32: sixteen times the tiles per rank even out the
-ranks' work (C3 at N=8: slowest rank 6.29 -> 5.96 ms, kernel-side bound 0.89 -> 0.94;
-profiles/r03z_rank_balance_tiles.log).
+plain t % world interleave no rank is tied to a fixed set of tile columns. The tile side follows
+the world size (tile_side): 8x8 (the primary lists' block) at N > 4, where many tiles per rank
+even out the ranks' work (C3 at N=8: slowest rank 6.29 -> 5.96 ms at round 3, kernel-side bound
+0.89 -> 0.94, profiles/r03z_rank_balance_tiles.log; 4.73 against 4.87 ms for 16x16 at round 4,
+profiles/r04zs_rank_balance_tiles.log); 16x16 at N = 2..4 and 32x32 at N = 1, where the waves that
+run at once cover a compact part of the image: at world 1 the 8x8 split renders C3 in 36.6 ms
+against 35.0 (16x16) and 34.9 (32x32, the plain path's 34.8; profiles/r04zs_split_tiles.log).
 The only exchange step is one gather of the finished slabs to rank 0 (torch.distributed:
 RCCL over xGMI on the GPU box, gloo in the CPU tests), after which rank 0 scatters the slabs
 into the ppmOut image (dt_unpack_slabs). Sample RNG is keyed on the global pixel index, so the
@@ -15,8 +18,15 @@ image is bit-identical for any world size.
 from . import DT_OUT_SLAB, slab_floats_max, tiles, unpack_slabs
 
 
+def tile_side(world):
+    """the split's tile side for a world size (module docstring)"""
+    return 32 if world <= 1 else 16 if world <= 4 else 8
+
+
 class FrameSplit:
-    def __init__(self, g, world, rank, tile_w=8, tile_h=8):
+    def __init__(self, g, world, rank, tile_w=None, tile_h=None):
+        tile_w = tile_w or tile_side(world)
+        tile_h = tile_h or tile_side(world)
         self.g = g
         self.world = world
         self.rank = rank

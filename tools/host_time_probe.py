@@ -14,11 +14,14 @@ import bench
 g, built = bench.build_globals(dt, "c3")
 dev = torch.device("cuda", 0)
 scene = dt.Scene(built, g)
-split = FrameSplit(g, 1, 0)
-slab = torch.zeros(split.slab_floats, dtype=torch.float32, device=dev)
 img = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device=dev)
 s = torch.cuda.current_stream(dev).cuda_stream
-for name, out, tile in (("plain", img, dt.tiles()), ("split", slab, split.tile)):
+cases = [("plain", img, dt.tiles())]
+for side in (8, 16, 32):   # FrameSplit's tile side (default 8)
+    split = FrameSplit(g, 1, 0, tile_w=side, tile_h=side)
+    cases.append(("split %dx%d" % (side, side), torch.zeros(split.slab_floats, dtype=torch.float32, device=dev),
+                  split.tile))
+for name, out, tile in cases:
     dt.render(scene, g, 240, out, tile); torch.cuda.synchronize()
     ts = []
     t0 = time.perf_counter()

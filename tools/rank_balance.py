@@ -4,7 +4,7 @@ trace-kernel time. With one GPU per rank the frame takes max_r T_r plus the gath
 T_1 / (N * max_r T_r) bounds the kernel-side strong-scaling efficiency of bench.py at N GPUs
 (load balance of the interleaved tiles, the persistent grid's tail on 1/N of the pixels).
 
-    python tools/rank_balance.py [c3|c2|c4] [reps]     (TILE=<side>: the split's tile side, default 8 as FrameSplit)
+    python tools/rank_balance.py [c3|c2|c4] [reps]     (TILE=<side>: the split's tile side, default FrameSplit's for the world size)
 
 INFLIGHT=n (2, 3, ...): each rank's time per frame over 16 frames rendered back to back on n streams with
 one scene object each (bench.py renders two in flight at N > 1), instead of one launch's kernel time.
@@ -46,11 +46,12 @@ def main():
             ms = (time.perf_counter() - t0) * 1e3 / 16
             best = ms if best is None else min(best, ms)
         return best
+    from distraytracer_amd.multigpu import tile_side
     t1 = None
     for world in (1, 2, 4, 8):
         per, work = [], []
         for rank in (range(world) if not os.environ.get("REVERSE") else reversed(range(world))):
-            ts = int(os.environ.get("TILE", "8"))   # tile side (FrameSplit: 8)
+            ts = int(os.environ["TILE"]) if "TILE" in os.environ else tile_side(world)   # as FrameSplit
             tile = dt.tiles(rank=rank, world=world, layout=dt.DT_OUT_SLAB, tile_w=ts, tile_h=ts)
             out = torch.zeros(max(dt.slab_floats(g, tile), 1), dtype=torch.float32, device="cuda")
             st = dt.render(scene, g, 240, out, tile)   # warm-up
