@@ -165,16 +165,19 @@ def counter_fp64(pmc, kernel_ms):
     return r
 
 
-def valu_roofline(cfg, kernel_ms, samples, ref_work=None, ref_samples=0, pmc=None):
+def valu_roofline(cfg, kernel_ms, samples, ref_work=None, ref_samples=0, pmc=None, world=1):
     """the binding roofline is the VALU. achieved = the include/dt_work.h events the
     trace kernel executes for this frame (counted by the diagnostic library in a child process) x
     their weights, / the trace kernel's HIP-event time; against the MI355X FP64 vector peak. Beside
     it: the counter-derived FP64 rate of the committed PMC profile (counter_fp64) and the reference
-    loop's count for the same frame (the oracle's, scaled from its sample)."""
+    loop's count for the same frame (the oracle's, scaled from its sample). At world > 1 the counting
+    run renders rank 0's share of the same split, so achieved is rank 0's GPU's rate on its share."""
     from distraytracer_amd import work as W
-    dev = W.device_counts(cfg)
+    dev = W.device_counts(cfg, world=world)
     if dev is None:
         return None
+    if world > 1:
+        samples = dev["samples"]   # rank 0's share of the timed frame, counted as the timed launch renders it
     ops = dev["ops"] * (samples / max(dev["samples"], 1))   # the counting frame is the timed frame
     achieved = ops / (kernel_ms / 1e3) / 1e12
     r = {"bound": "valu", "achieved": round(achieved, 4), "peak": W.PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
@@ -184,7 +187,9 @@ def valu_roofline(cfg, kernel_ms, samples, ref_work=None, ref_samples=0, pmc=Non
          "counts_per_sample": W.breakdown(dev["counts"], dev["samples"]),
          "note": "FP64-equivalent VALU operations of the events the kernel executes (include/dt_work.h "
                  "weights x libdt_work.so counts) / the trace kernel's HIP-event time, against the "
-                 "78.6 TFLOP/s FP64 vector peak (an FMA counts 2 there and in counter_fp64)"}
+                 "78.6 TFLOP/s FP64 vector peak (an FMA counts 2 there and in counter_fp64)",
+         "share": ("rank 0's share of a %d-way tile split (%d pixel-samples per frame)" % (world, samples)
+                   if world > 1 else "the whole frame")}
     cf = counter_fp64(pmc, kernel_ms)
     if cf is not None:
         cf["ratio_to_weighted"] = round(cf["achieved"] / achieved, 4) if achieved else None
@@ -320,7 +325,19 @@ def main():
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    if len(scenes) > 1:
+        # two frames in flight on alternating streams: a frame's own event pair also spans the time
+        # its waves share the GPU with the other stream's frame (the pairs summed exceed the step
+        # time), so the kernel time per frame is the span from the first frame's start to the last
+        # end, / K: the GPU time the K launches occupy, never above ms_per_step
+        start = min(evs[0][0].elapsed_time(a) for a, _ in evs)
+        end = max(evs[0][0].elapsed_time(b) for _, b in evs)
+        kernel_ms = (end - start) / args.steps
+        kernel_basis = "span of the %d launches / %d (two frames in flight on alternating streams)" % (
+            args.steps, args.steps)
+    else:
+        kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+        kernel_basis = "mean of the %d launches' HIP-event durations on the launch stream" % args.steps
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -351,13 +368,18 @@ def main():
             cpu, parity, ref_work, ref_samples = cpu_baseline(dt, args.config, args.cpu_frac, scene, dev,
                                                               args.cpu_all_cores)
         roof = None
-        if world == 1 and not args.no_roofline:
+        if not args.no_roofline:
+            # at N > 1 the work is counted on rank 0's share of the split (the frame this GPU renders);
+            # the committed PMC profile is of a whole-frame launch, so counter_fp64 is N = 1 only
             roof = valu_roofline(args.config, kernel_ms, W * H * spp, ref_work, ref_samples,
-                                 pmc if pmc.get("kernel") == trace_kernel_name(spp, g.use_model) else None)
+                                 pmc if world == 1 and pmc.get("kernel") == trace_kernel_name(spp, g.use_model)
+                                 else None, world=world)
         if roof is not None:
             roof["kernel"] = trace_kernel_name(spp, g.use_model)
-        if roof is None:   # no diagnostic library (or N > 1): the HBM line alone
-            roof = dict(hbm, kernel=trace_kernel_name(spp, g.use_model), kernel_ms=round(kernel_ms, 3))
+            roof["kernel_ms_basis"] = kernel_basis
+        if roof is None:   # no diagnostic library: the HBM line alone
+            roof = dict(hbm, kernel=trace_kernel_name(spp, g.use_model), kernel_ms=round(kernel_ms, 3),
+                        kernel_ms_basis=kernel_basis)
         else:
             roof["hbm"] = hbm
         if pmc.get("valu_active_per_wave_cycle"):

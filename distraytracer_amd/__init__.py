@@ -68,6 +68,17 @@ def accel_info(built, g):
     return info.as_dict()
 
 
+def trace_build(built, g, frame):
+    """The trace-kernel build dt_render launches for (built, g) at `frame` (automatic choice, host
+    only, dt_trace_build): (kernel name, the scene's feature mask, the build's feature mask)."""
+    name = ctypes.create_string_buffer(64)
+    sf, bf = ctypes.c_uint32(), ctypes.c_uint32()
+    desc = built._ptr if isinstance(built, BuiltScene) else ctypes.pointer(built)
+    check(lib.dt_trace_build(desc, ctypes.byref(g), int(frame), name, 64, ctypes.byref(sf), ctypes.byref(bf)),
+          "dt_trace_build")
+    return name.value.decode(), sf.value, bf.value
+
+
 class Scene:
     """Device-resident scene + reference-topology BVH (dt_scene_create). upload=False runs only the
     host half (dt_scene_prepare: no device work, safe beside a running render); upload() or the

@@ -23,7 +23,7 @@ DT_KERNEL_AUTO, DT_KERNEL_PRODUCT, DT_KERNEL_DONATE = 0, 1, 2   # dt_scene_set_k
 
 SHAPE_TYPES = {1: "sphere", 2: "cylinder", 3: "triangle", 4: "rectangle", 5: "rectprism_v2",
                6: "checkerboard", 7: "checkerboard_hole", 8: "checker_cylinder", 9: "rectprism_cyl"}
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class ShapeDesc(ctypes.Structure):
@@ -115,7 +115,7 @@ class AccelInfo(ctypes.Structure):
 # every symbol include/dt.h declares (checked by tests/test_abi.py)
 EXPORTS = ["dt_abi_version", "dt_last_error", "dt_globals_default", "dt_scene_create", "dt_scene_destroy",
            "dt_scene_prepare", "dt_scene_upload", "dt_scene_set_kernel",
-           "dt_scene_bvh", "dt_bvh_build", "dt_accel_info_build", "dt_slab_floats", "dt_slab_floats_max",
+           "dt_scene_bvh", "dt_bvh_build", "dt_accel_info_build", "dt_trace_build", "dt_slab_floats", "dt_slab_floats_max",
            "dt_render", "dt_render_async", "dt_collect_stats", "dt_debug_counters", "dt_render_sky",
            "dt_unpack_slabs", "dt_build_scene", "dt_scene_desc_free", "dt_write_ppm", "dt_write_png",
            "dt_mocap_bone_table", "dt_debug_normalize", "dt_intersect_primary",
@@ -163,6 +163,8 @@ def _load():
         "dt_bvh_build": (c_int32, [P(SceneDesc), P(Globals), P(BVHNode), c_int32, P(c_int32), c_int32, P(c_int32),
                                    P(c_int32)]),
         "dt_accel_info_build": (c_int32, [P(SceneDesc), P(Globals), P(AccelInfo)]),
+        "dt_trace_build": (c_int32, [P(SceneDesc), P(Globals), c_int32, ctypes.c_char_p, c_int32,
+                                     P(ctypes.c_uint32), P(ctypes.c_uint32)]),
         "dt_slab_floats": (c_int64, [P(Globals), P(Tiles)]),
         "dt_slab_floats_max": (c_int64, [P(Globals), P(Tiles)]),
         "dt_render": (c_int32, [ctypes.c_void_p, P(Globals), c_int32, P(Tiles), ctypes.c_void_p, c_int32,

@@ -690,6 +690,91 @@ static void fill_hscene(const dt_scene* sc, HScene& hs)
   hs.pl_list = (const uint32_t*)sc->d_pl_list;
 }
 
+// The trace-kernel builds (dt_kernels.hip DT_TRACE_KERNEL, Makefile TRACE_BUILDS) and the choice
+// of one per render.
+struct Build {
+  hipError_t (*launch)(const void*, float*, int, hipStream_t);
+  const void* (*ptr)(void);
+  int (*traits)(void);
+  const char* name;
+  int resident;
+};
+#define DT_B(k) {k##_launch, k##_ptr, k##_traits, #k, 0}
+// per wave count (4, 5): room, mesh, full (still frames); tunnel, blur (motion-blur frames); sky
+static Build g_builds[2][6] = {
+    {DT_B(dt_trace_kernel), DT_B(dt_trace_kernel_mesh), DT_B(dt_trace_kernel_full),
+     DT_B(dt_trace_kernel_tunnel), DT_B(dt_trace_kernel_blur), DT_B(dt_trace_kernel_sky)},
+    {DT_B(dt_trace_kernel_w5), DT_B(dt_trace_kernel_w5_mesh), DT_B(dt_trace_kernel_w5_full),
+     DT_B(dt_trace_kernel_w5_tunnel), DT_B(dt_trace_kernel_w5_blur), DT_B(dt_trace_kernel_w5_sky)}};
+static Build g_dn_build = DT_B(dt_trace_kernel_dn), g_rpc_build = DT_B(dt_trace_kernel_rpc);
+#undef DT_B
+
+// the feature mask a build was compiled for (its traits' bits 8..23: dt_kernels.hip DT_FEATURES)
+static unsigned build_features(const Build& b) { return ((unsigned)b.traits() >> 8) & 0xFFFFu; }
+// the *_sky build of the same wave count as the product build b (it renders b's sky items)
+static Build& sky_build_for(const Build& b)
+{
+  for (int v = 0; v < 6; ++v)
+    if (&b == &g_builds[1][v]) return g_builds[1][5];
+  return g_builds[0][5];
+}
+
+// The build a render of a scene with these features launches (kernel_choice: dt_scene_set_kernel).
+static Build& choose_build(unsigned scene_features, bool no_cull, int kernel_choice, const dtd::DParams& P)
+{
+  // scenes with a RectPrismWithCylinder take the trace kernel compiled with its tests (dt_kernels.hip
+  // DT_WITH_RPC), whose occupancy may differ. DFS work sharing inside the wave (dt_trace_kernel_dn)
+  // when DT_DONATE=1; its pre-order paths hold 10 levels of 3 bits (max_depth <= 11, brdf_samples <= 6)
+  // (dt_scene_set_kernel; DT_KERNEL_AUTO: the DT_DONATE environment variable)
+  const char* dn_env = kernel_choice == DT_KERNEL_AUTO ? getenv("DT_DONATE") : nullptr;
+  const bool want_dn = kernel_choice == DT_KERNEL_DONATE || (dn_env && dn_env[0] == '1');
+  const bool donate = !no_cull && want_dn && P.max_depth <= 11 && P.brdf_samples <= 6;
+  if (no_cull) return g_rpc_build;
+  if (donate) return g_dn_build;
+  // one pixel per wave (spp >= 64) takes the 5-waves-per-SIMD build (dt_kernels.hip DT_W5): C3 +1.8%,
+  // C4 +4%; with several pixels per wave (C2, 16 spp) it loses 8% (profiles/r03ba_ab_w5.log).
+  // DT_W5=0 never, DT_W5=1 at any spp with at most 8 pixels per wave (its per-pixel sums have 8 slots).
+  const char* w5_env = getenv("DT_W5");
+  const bool w5 = P.ppw <= 8 && (w5_env ? w5_env[0] == '1' : P.spp >= 64);
+  // below frame_prism every motion-blur pass shifts by 0 (the reference's val, Q19), so those frames
+  // take the product kernels built without the shift paths (dt_kernels.hip DT_NOSHIFT), room scenes
+  // the builds without the shape types, lights and materials they lack (DT_FEATURES); later frames
+  // the *_blur builds (DT_BLUR_KERNEL=1: those for every frame, the tests' check of the builds
+  // against each other)
+  const char* bk_env = getenv("DT_BLUR_KERNEL");
+  const bool blur = P.frame >= P.frame_prism || (bk_env && bk_env[0] == '1');
+  // DT_FULL_KERNEL=1: the builds with every feature for any scene (the tests' check of the
+  // feature builds against them)
+  const char* fk_env = getenv("DT_FULL_KERNEL");
+  const unsigned feats = fk_env && fk_env[0] == '1' ? ~0u : scene_features;
+  auto within = [&](unsigned mask) { return (feats & ~mask) == 0; };
+  const int variant = blur ? (within(DT_TUNNEL_FEATURES) ? 3 : 4)
+                           : within(DT_ROOM_FEATURES) ? 0 : within(DT_MESH_FEATURES) ? 1 : 2;
+  return g_builds[w5 ? 1 : 0][variant];
+}
+
+int dt_trace_build(const dt_scene_desc* desc, const dt_globals* g, int32_t frame, char* name, int32_t name_cap,
+                   uint32_t* scene_feats, uint32_t* build_feats)
+{
+  if (!desc || !g) return fail(DT_E_INVALID, "null argument");
+  if (desc->n_shapes < 0 || (desc->n_shapes > 0 && !desc->shapes)) return fail(DT_E_INVALID, "invalid descriptor");
+  dtd::DParams P;
+  std::string err;
+  int rc = fill_params(*g, frame, nullptr, P, err);
+  if (rc) return fail(rc, err);
+  bool no_cull = false;   // as build_accel: a RectPrismWithCylinder takes the rpc build
+  for (int i = 0; i < desc->n_shapes; ++i) no_cull |= desc->shapes[i].type == DT_SHAPE_RECTPRISM_CYL;
+  const unsigned f = scene_features(*desc);
+  const Build& b = choose_build(f, no_cull, DT_KERNEL_AUTO, P);
+  if (name && name_cap > 0) {
+    strncpy(name, b.name, (size_t)name_cap - 1);
+    name[name_cap - 1] = 0;
+  }
+  if (scene_feats) *scene_feats = f;
+  if (build_feats) *build_feats = build_features(b);
+  return DT_OK;
+}
+
 static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>& zs, float* out_dev,
                           hipStream_t st)
 {
@@ -713,50 +798,14 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   hs.cloud_z = (const float*)sc->d_zs;
   hs.stats = sc->d_stats;
   hs.queue = sc->d_stats + ST_N;
-  // scenes with a RectPrismWithCylinder take the trace kernel compiled with its tests (dt_kernels.hip
-  // DT_WITH_RPC), whose occupancy may differ. DFS work sharing inside the wave (dt_trace_kernel_dn)
-  // when DT_DONATE=1; its pre-order paths hold 10 levels of 3 bits (max_depth <= 11, brdf_samples <= 6)
-  // (dt_scene_set_kernel; DT_KERNEL_AUTO: the DT_DONATE environment variable)
-  const char* dn_env = sc->kernel == DT_KERNEL_AUTO ? getenv("DT_DONATE") : nullptr;
-  const bool want_dn = sc->kernel == DT_KERNEL_DONATE || (dn_env && dn_env[0] == '1');
-  const bool donate = !sc->no_cull && want_dn && P.max_depth <= 11 && P.brdf_samples <= 6;
-  // one pixel per wave (spp >= 64) takes the 5-waves-per-SIMD build (dt_kernels.hip DT_W5): C3 +1.8%,
-  // C4 +4%; with several pixels per wave (C2, 16 spp) it loses 8% (profiles/r03ba_ab_w5.log).
-  // DT_W5=0 never, DT_W5=1 at any spp with at most 8 pixels per wave (its per-pixel sums have 8 slots).
-  const char* w5_env = getenv("DT_W5");
-  const bool w5 = !sc->no_cull && !donate && P.ppw <= 8 && (w5_env ? w5_env[0] == '1' : P.spp >= 64);
-  // below frame_prism every motion-blur pass shifts by 0 (the reference's val, Q19), so those frames
-  // take the product kernels built without the shift paths (dt_kernels.hip DT_NOSHIFT), room scenes
-  // the builds without the shape types, lights and materials they lack (DT_FEATURES); later frames
-  // the *_blur builds (DT_BLUR_KERNEL=1: those for every frame, the tests' check of the builds
-  // against each other)
-  const char* bk_env = getenv("DT_BLUR_KERNEL");
-  const bool blur = P.frame >= P.frame_prism || (bk_env && bk_env[0] == '1');
-  struct Build {
-    hipError_t (*launch)(const void*, float*, int, hipStream_t);
-    const void* (*ptr)(void);
-    int (*traits)(void);
-    int resident;
-  };
-#define DT_B(k) {k##_launch, k##_ptr, k##_traits, 0}
-  // per wave count (4, 5): room, mesh, full (still frames); tunnel, blur (motion-blur frames); sky
-  static Build builds[2][6] = {
-      {DT_B(dt_trace_kernel), DT_B(dt_trace_kernel_mesh), DT_B(dt_trace_kernel_full),
-       DT_B(dt_trace_kernel_tunnel), DT_B(dt_trace_kernel_blur), DT_B(dt_trace_kernel_sky)},
-      {DT_B(dt_trace_kernel_w5), DT_B(dt_trace_kernel_w5_mesh), DT_B(dt_trace_kernel_w5_full),
-       DT_B(dt_trace_kernel_w5_tunnel), DT_B(dt_trace_kernel_w5_blur), DT_B(dt_trace_kernel_w5_sky)}};
-  static Build dn_build = DT_B(dt_trace_kernel_dn), rpc_build = DT_B(dt_trace_kernel_rpc);
-#undef DT_B
-  // DT_FULL_KERNEL=1: the builds with every feature for any scene (the tests' check of the
-  // feature builds against them)
-  const char* fk_env = getenv("DT_FULL_KERNEL");
-  const unsigned feats = fk_env && fk_env[0] == '1' ? ~0u : sc->features;
-  auto within = [&](unsigned mask) { return (feats & ~mask) == 0; };
-  const int variant = blur ? (within(DT_TUNNEL_FEATURES) ? 3 : 4)
-                           : within(DT_ROOM_FEATURES) ? 0 : within(DT_MESH_FEATURES) ? 1 : 2;
-  Build* const wb = builds[w5 ? 1 : 0];
-  Build& kb = sc->no_cull ? rpc_build : donate ? dn_build : wb[variant];
-  Build& kb2 = wb[5];   // the *_sky build of the same wave count: renders the sky items
+  const int kernel_choice = sc->kernel;
+  Build& kb = choose_build(sc->features, sc->no_cull, kernel_choice, P);
+  const bool donate = &kb == &g_dn_build;
+  Build& kb2 = sky_build_for(kb);
+  // the build must handle every feature of the scene: its DT_FEATURES compile the others out to
+  // __builtin_unreachable() (tests/test_host.py checks every builder scene; this guards the rest)
+  if (sc->features & ~build_features(kb))
+    return fail(DT_E_INVALID, "no trace-kernel build covers the scene's features");
   if (!kb.resident) kb.resident = max_resident_waves(kb.ptr(), 64);
   const int64_t waves = kb.resident;
   int64_t grid = P.n_items < waves ? P.n_items : waves;
@@ -823,10 +872,26 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   hs.again_list = nullptr;
   hs.again_n = nullptr;
   if (again) {
-    if (!sc->d_stats2) {
-      HIPCHK(hipMalloc((void**)&sc->d_stats2, sizeof(unsigned long long) * (ST_N + 2)));
-      HIPCHK(hipMalloc(&sc->d_launch2, dt_launch_size()));
-      HIPCHK(hipHostMalloc((void**)&sc->h_launch2, dt_launch_size(), hipHostMallocDefault));
+    if (!sc->d_stats2 || !sc->d_launch2 || !sc->h_launch2) {
+      // all three or none: allocated into temporaries, committed together, freed on a failure
+      unsigned long long* st2 = nullptr;
+      void* dl2 = nullptr;
+      uint8_t* hl2 = nullptr;
+      hipError_t e = hipMalloc((void**)&st2, sizeof(unsigned long long) * (ST_N + 2));
+      if (e == hipSuccess) e = hipMalloc(&dl2, dt_launch_size());
+      if (e == hipSuccess) e = hipHostMalloc((void**)&hl2, dt_launch_size(), hipHostMallocDefault);
+      if (e != hipSuccess) {
+        if (st2) (void)hipFree(st2);
+        if (dl2) (void)hipFree(dl2);
+        if (hl2) (void)hipHostFree(hl2);
+        return fail(DT_E_NO_DEVICE, std::string("sky-item launch buffers: ") + hipGetErrorString(e));
+      }
+      if (sc->d_stats2) (void)hipFree(sc->d_stats2);
+      if (sc->d_launch2) (void)hipFree(sc->d_launch2);
+      if (sc->h_launch2) (void)hipHostFree(sc->h_launch2);
+      sc->d_stats2 = st2;
+      sc->d_launch2 = dl2;
+      sc->h_launch2 = hl2;
     }
     if (PL.n_items > sc->again_cap) {
       HIPCHK(hipStreamSynchronize(st));

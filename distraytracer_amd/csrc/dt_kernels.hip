@@ -398,9 +398,35 @@ __device__ V3 cloud_finish(const DParams& P, V3 color)
 #define DT_CLOUD_ABOVE 1.3126
 #define DT_CLOUD_BELOW (-2.3126)
 
+// DT_SKY_CALL=1 (diagnostic builds only, tools/call_repro): the two cloudColor entry points below
+// emitted as real calls instead of inlined, to study the called-march defect
+#ifndef DT_SKY_CALL
+#define DT_SKY_CALL 0
+#endif
+#if DT_SKY_CALL
+#define DT_SKY_FN __noinline__
+// the callee checks its workitem id (threadIdx.x, an implicit input of a call) against the lane id
+// from v_mbcnt (no input): mismatches are counted in dt_stats.donate_overflow (unused outside the
+// work-sharing build). DT_SKY_CALL=2 takes the cooperative march's lane from v_mbcnt.
+#define DT_SKY_DBG , unsigned long long* __restrict__ dbg
+#define DT_SKY_DBG_ARG(p) , (p)
+#define DT_SKY_TID_CHECK() do { if ((int)(threadIdx.x & 63) != (int)__lane_id()) atomicAdd(dbg, 1ull); } while (0)
+#else
+#define DT_SKY_FN __forceinline__
+#define DT_SKY_DBG
+#define DT_SKY_DBG_ARG(p)
+#define DT_SKY_TID_CHECK() do { } while (0)
+#endif
+#if DT_SKY_CALL == 2
+#define DT_SKY_LANE() ((int)__lane_id())
+#else
+#define DT_SKY_LANE() ((int)(threadIdx.x & 63))
+#endif
+
 // full cloudColor on one lane
-__device__ __forceinline__ V3 cloud_color_lane(const DParams& P, const float* __restrict__ zs, V3 ray)
+__device__ DT_SKY_FN V3 cloud_color_lane(const DParams& P, const float* __restrict__ zs, V3 ray DT_SKY_DBG)
 {
+  DT_SKY_TID_CHECK();
   V3 sky = sky_color(P, ray);
   V3 color = sky;
   for (int s = 0; s < P.n_cloud_steps; ++s) {
@@ -420,12 +446,13 @@ __device__ __forceinline__ V3 cloud_color_lane(const DParams& P, const float* __
 // cloudColor for one (wave-uniform) ray computed by all 64 lanes: the march steps are
 // spread over lanes (the noise is 99% of the work), the per-channel recurrence then runs
 // on lanes 0..2 in step order, so every addition happens in the reference's order.
-__device__ __forceinline__ V3 cloud_color_coop(const DParams& P, const float* __restrict__ zs, V3 ray,
-                               float* __restrict__ dens, double* __restrict__ chan)
+__device__ DT_SKY_FN V3 cloud_color_coop(const DParams& P, const float* __restrict__ zs, V3 ray,
+                               float* __restrict__ dens, double* __restrict__ chan DT_SKY_DBG)
 {
   // the march in chunks of DT_CLOUD_CHUNK steps: densities in parallel over the lanes, then
   // the per-channel recurrence on lanes 0-2 in step order (same arithmetic as one pass)
-  const int lane = threadIdx.x & 63;
+  DT_SKY_TID_CHECK();
+  const int lane = DT_SKY_LANE();
   V3 sky = sky_color(P, ray);
   double c = lane == 0 ? sky.x : (lane == 1 ? sky.y : sky.z);
   const double rev = lane == 0 ? sky.z : (lane == 1 ? sky.y : sky.x);
@@ -3051,7 +3078,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
             pt.x = ((P.sky_m[0][0] * fp.x + P.sky_m[0][1] * fp.y) + P.sky_m[0][2] * fp.z) + P.sky_m[0][3] * 1.0;
             pt.y = ((P.sky_m[1][0] * fp.x + P.sky_m[1][1] * fp.y) + P.sky_m[1][2] * fp.z) + P.sky_m[1][3] * 1.0;
             pt.z = ((P.sky_m[2][0] * fp.x + P.sky_m[2][1] * fp.y) + P.sky_m[2][2] * fp.z) + P.sky_m[2][3] * 1.0;
-            V3 skyc = cloud_color_coop(P, S.cloud_z, pt, dens, chan);
+            V3 skyc = cloud_color_coop(P, S.cloud_z, pt, dens, chan DT_SKY_DBG_ARG(S.stats + ST_DN_OVF));
             if (miss && j == jj) tmp_color = skyc;
             if (lane == 0) sky_px++;
           }
@@ -3182,7 +3209,7 @@ dt_sky_miss_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     pt.x = ((P.sky_m[0][0] * fp.x + P.sky_m[0][1] * fp.y) + P.sky_m[0][2] * fp.z) + P.sky_m[0][3] * 1.0;
     pt.y = ((P.sky_m[1][0] * fp.x + P.sky_m[1][1] * fp.y) + P.sky_m[1][2] * fp.z) + P.sky_m[1][3] * 1.0;
     pt.z = ((P.sky_m[2][0] * fp.x + P.sky_m[2][1] * fp.y) + P.sky_m[2][2] * fp.z) + P.sky_m[2][3] * 1.0;
-    const V3 color = cloud_color_lane(P, S.cloud_z, pt);
+    const V3 color = cloud_color_lane(P, S.cloud_z, pt DT_SKY_DBG_ARG(S.stats + ST_DN_OVF));
     if (valid) {
       store_pixel(P, out, x, y, so, color);
       if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
@@ -3215,7 +3242,7 @@ dt_sky_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   pt.x = ((P.sky_m[0][0] * fp.x + P.sky_m[0][1] * fp.y) + P.sky_m[0][2] * fp.z) + P.sky_m[0][3] * 1.0;
   pt.y = ((P.sky_m[1][0] * fp.x + P.sky_m[1][1] * fp.y) + P.sky_m[1][2] * fp.z) + P.sky_m[1][3] * 1.0;
   pt.z = ((P.sky_m[2][0] * fp.x + P.sky_m[2][1] * fp.y) + P.sky_m[2][2] * fp.z) + P.sky_m[2][3] * 1.0;
-  V3 color = cloud_color_lane(P, zs, pt);
+  V3 color = cloud_color_lane(P, zs, pt DT_SKY_DBG_ARG(Lp->S.stats + ST_DN_OVF));
   store_pixel(P, out, x, y, so, color);
 }
 
@@ -3306,6 +3333,10 @@ extern "C" hipError_t DT_CAT(DT_TRACE_KERNEL, _launch)(const void* dev_launch, f
   return hipGetLastError();
 }
 extern "C" const void* DT_CAT(DT_TRACE_KERNEL, _ptr)(void) { return (const void*)DT_TRACE_KERNEL; }
-// bit 0: the build lists sky items for another launch (DT_SKY_AGAIN)
-extern "C" int DT_CAT(DT_TRACE_KERNEL, _traits)(void) { return DT_SKY_AGAIN ? 1 : 0; }
+// bit 0: the build lists sky items for another launch (DT_SKY_AGAIN); bits 8..23: the scene features
+// it handles (DT_FEATURES; dt_api.cpp launches it only for scenes within them)
+extern "C" int DT_CAT(DT_TRACE_KERNEL, _traits)(void)
+{
+  return (DT_SKY_AGAIN ? 1 : 0) | (int)(((DT_FEATURES) & 0xFFFFu) << 8);
+}
 #endif

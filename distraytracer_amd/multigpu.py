@@ -4,12 +4,13 @@ Every rank holds the whole (tiny) scene and renders one tile of every group of `
 consecutive tiles (raster order), the ranks rotated by a hash of the group (dt_scene_dev.h
 tile_of), into a packed slab: the expensive sky/glossy regions spread over all GPUs, and unlike a
 plain t % world interleave no rank is tied to a fixed set of tile columns. The tile side follows
-the world size (tile_side): 8x8 (the primary lists' block) at N > 4, where many tiles per rank
-even out the ranks' work (C3 at N=8: slowest rank 6.29 -> 5.96 ms at round 3, kernel-side bound
-0.89 -> 0.94, profiles/r03z_rank_balance_tiles.log; 4.73 against 4.87 ms for 16x16 at round 4,
-profiles/r04zs_rank_balance_tiles.log); 16x16 at N = 2..4 and 32x32 at N = 1, where the waves that
-run at once cover a compact part of the image: at world 1 the 8x8 split renders C3 in 36.6 ms
-against 35.0 (16x16) and 34.9 (32x32, the plain path's 34.8; profiles/r04zs_split_tiles.log).
+the world size (tile_side): 8x8 (the primary lists' block) at every N > 1, where many tiles per
+rank even out the ranks' work. Rank-balance kernel times of C3 (profiles/r04zs_rank_balance_tiles.log,
+slowest share 8x8 against 16x16): N=2 17.60 against 17.75 ms, N=4 9.09 against 9.12, N=8 4.73
+against 4.87 (round 3: slowest rank 6.29 -> 5.96 ms from 32x32, profiles/r03z_rank_balance_tiles.log).
+32x32 at N = 1, where the waves that run at once cover a compact part of the image: at world 1 the
+8x8 split renders C3 in 36.6 ms against 35.0 (16x16) and 34.9 (32x32, the plain path's 34.8;
+profiles/r04zs_split_tiles.log).
 The only exchange step is one gather of the finished slabs to rank 0 (torch.distributed:
 RCCL over xGMI on the GPU box, gloo in the CPU tests), after which rank 0 scatters the slabs
 into the ppmOut image (dt_unpack_slabs). Sample RNG is keyed on the global pixel index, so the
@@ -20,7 +21,7 @@ from . import DT_OUT_SLAB, slab_floats_max, tiles, unpack_slabs
 
 def tile_side(world):
     """the split's tile side for a world size (module docstring)"""
-    return 32 if world <= 1 else 16 if world <= 4 else 8
+    return 32 if world <= 1 else 8
 
 
 class FrameSplit:
@@ -126,32 +127,39 @@ class FrameQueue:
     store counter is a host-side atomic add.
 
     frames: the frame ids to render; cost: {frame id: estimated cost} (missing ids: the mean);
-    store: a torch.distributed Store (None: a single process, plain iteration)."""
+    store: a torch.distributed Store (None: a single process, plain iteration); key, epoch: the
+    store keys of this queue, the same on every rank (a second pass or a retry in the same process
+    group passes another epoch, so its counter starts at 0); rank, world: this process's place in
+    the group (default: torch.distributed's)."""
 
-    _instances = 0   # queues made in this process: every rank makes them in the same sequence
-
-    def __init__(self, frames, cost=None, store=None, key="dt_frame_queue"):
+    def __init__(self, frames, cost=None, store=None, key="dt_frame_queue", epoch=0, rank=None, world=None):
         cost = cost or {}
         known = [cost[n] for n in frames if n in cost]
         mean = sum(known) / len(known) if known else 1.0
         # stable: equal costs keep the frames' own order
         self.order = sorted(frames, key=lambda n: -cost.get(n, mean))
         self.store = store
-        # a fresh counter per queue (a second pass or a retry in the same process group starts at
-        # 0, not past the end of the previous queue's counter)
-        self.key = "%s/%d" % (key, FrameQueue._instances)
-        FrameQueue._instances += 1
+        self.key = "%s/%d" % (key, epoch)
         self._local = 0
         if store is not None:
+            if rank is None or world is None:
+                import torch.distributed as dist
+                rank = dist.get_rank() if rank is None else rank
+                world = dist.get_world_size() if world is None else world
             # every rank must hand out the same order, or frames would be rendered twice or never:
-            # the first rank stores a hash of its order, the others must find the same one
+            # each rank publishes a hash of its order, waits for every rank's and compares them all,
+            # so on a mismatch every rank raises (none goes on rendering)
             import hashlib
             h = hashlib.sha1(repr(self.order).encode()).hexdigest()
-            got = store.compare_set(self.key + "/order", "", h)
-            got = got.decode() if isinstance(got, bytes) else got
-            if got != h:
-                raise RuntimeError("FrameQueue %s: this rank's frame order differs from another rank's "
-                                   "(different frame lists or cost data)" % self.key)
+            store.set("%s/order/%d" % (self.key, rank), h)
+            keys = ["%s/order/%d" % (self.key, r) for r in range(world)]
+            store.wait(keys)
+            hashes = [store.get(k) for k in keys]
+            hashes = [x.decode() if isinstance(x, bytes) else x for x in hashes]
+            bad = [r for r, x in enumerate(hashes) if x != h]
+            if bad:
+                raise RuntimeError("FrameQueue %s: rank %d's frame order differs from rank(s) %s "
+                                   "(different frame lists or cost data)" % (self.key, rank, bad))
 
     def next(self):
         """the next frame id, or None when every frame has been handed out"""

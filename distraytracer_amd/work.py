@@ -69,13 +69,19 @@ def breakdown(counts, samples):
     return out
 
 
-def device_counts(config, timeout=180):
+def device_counts(config, timeout=180, world=1):
     """Per-event counts of one frame of `config` executed by the diagnostic kernels (child process
-    with DT_LIB=libdt_work.so). None when the diagnostic library was not built."""
+    with DT_LIB=libdt_work.so); world > 1: of rank 0's share of the frame's tile split
+    (multigpu.FrameSplit, as bench.py renders it). None when the diagnostic library was not built."""
     if not os.path.exists(WORK_LIB):
         return None
-    env = dict(os.environ, DT_LIB=WORK_LIB)
-    r = subprocess.run([sys.executable, "-m", "distraytracer_amd.work", "--config", config], env=env,
+    # the child renders alone on this process's GPU: no torch.distributed rendezvous variables
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "MASTER_ADDR",
+                        "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    env["DT_LIB"] = WORK_LIB
+    r = subprocess.run([sys.executable, "-m", "distraytracer_amd.work", "--config", config,
+                        "--world", str(world)], env=env,
                        cwd=os.path.dirname(_HERE), capture_output=True, text=True, timeout=timeout)
     if r.returncode != 0:
         raise RuntimeError("work counting failed: %s" % r.stderr[-2000:])
@@ -91,6 +97,7 @@ def _count_main():
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
+    ap.add_argument("--world", type=int, default=1, help="count rank 0's share of a WORLD-way tile split")
     args = ap.parse_args()
     sys.path.insert(0, os.path.dirname(_HERE))
     import bench
@@ -101,14 +108,20 @@ def _count_main():
     torch.cuda.set_device(0)
     g, built = bench.build_globals(dt, args.config)
     scene = dt.Scene(built, g)
-    out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
-    st = dt.render(scene, g, 240, out, dt.tiles())
+    if args.world > 1:
+        from distraytracer_amd.multigpu import FrameSplit
+        split = FrameSplit(g, args.world, 0)
+        out = torch.zeros(split.slab_floats, dtype=torch.float32, device="cuda")
+        st = dt.render(scene, g, 240, out, split.tile)
+    else:
+        out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
+        st = dt.render(scene, g, 240, out, dt.tiles())
     buf = (ctypes.c_uint64 * N_EVENTS)()
     dt.check(dt.lib.dt_debug_counters(scene.handle, buf, N_EVENTS), "dt_debug_counters")
     counts = np.array(list(buf), dtype=np.float64)
     counts[SKY] = st.sky_pixels   # the sky is marched once per pixel, cooperatively or per lane
     scene.close()
-    print(json.dumps({"config": args.config, "samples": int(st.samples), "pixels": int(st.pixels),
+    print(json.dumps({"config": args.config, "world": args.world, "samples": int(st.samples), "pixels": int(st.pixels),
                       "rays": int(st.rays), "shadow_rays": int(st.shadow_rays), "sky_pixels": int(st.sky_pixels),
                       "counts": [int(c) for c in counts], "ops": price(counts),
                       "diagnostic_kernel_ms": round(st.kernel_ms, 3)}))

@@ -42,7 +42,8 @@ extern "C" {
 /* 3: dt_stats.donations / donate_overflow (DFS work sharing inside a wave, DT_DONATE) */
 /* 4: dt_scene_set_kernel (the trace-kernel choice per scene, not through the environment) */
 /* 5: dt_accel_info.features */
-#define DT_ABI_VERSION 5
+/* 6: dt_trace_build (the trace-kernel build a render launches, and the features it covers) */
+#define DT_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------- */
 #define DT_OK              0
@@ -310,6 +311,16 @@ typedef struct dt_accel_info {
                                   lights/emitters (the build dt_render launches) */
 } dt_accel_info;
 int dt_accel_info_build(const dt_scene_desc* desc, const dt_globals* g, dt_accel_info* info);
+
+/* The trace-kernel build dt_render launches for (desc, g) at `frame` with the automatic kernel
+ * choice (the DT_* environment switches apply as in dt_render), decided on the host only (no
+ * device): its kernel name (NUL-terminated, truncated to name_cap), the scene's feature mask (as
+ * dt_accel_info.features) and the mask the build was compiled for (dt_kernels.hip DT_FEATURES).
+ * dt_render refuses (DT_E_INVALID) a scene with a feature outside its build's mask rather than
+ * launching code that has that case compiled out. No reference counterpart: the reference has one
+ * CPU render loop (render_final_project.cpp:965-1222). */
+int dt_trace_build(const dt_scene_desc* desc, const dt_globals* g, int32_t frame, char* name, int32_t name_cap,
+                   uint32_t* scene_features, uint32_t* build_features);
 
 /* number of floats a DT_OUT_SLAB output needs for (g, tiles) */
 int64_t dt_slab_floats(const dt_globals* g, const dt_tiles* tiles);

@@ -123,13 +123,13 @@ def _queue_worker(rank, world, port, result_path):
         store = dist.distributed_c10d._get_default_store()
         frames = list(range(0, 40, 2))
         cost = {n: float(n % 7 + (50 if n == 24 else 0)) for n in frames}
-        q = FrameQueue(frames, cost, store)
+        q = FrameQueue(frames, cost, store, epoch=0, rank=rank, world=world)
         got = []
         for n in q:
             got.append(n)
             time.sleep(0.002 * cost[n])   # "render": a rank holding a costly frame takes fewer
         # a second queue in the same process group (a second animation pass) starts afresh
-        q2 = FrameQueue(list(range(5)), None, store)
+        q2 = FrameQueue(list(range(5)), None, store, epoch=1, rank=rank, world=world)
         got2 = list(q2)
         everyone = [None] * world
         dist.all_gather_object(everyone, [got, got2])
@@ -137,7 +137,7 @@ def _queue_worker(rank, world, port, result_path):
         bad_cost = {n: float(n if rank == 1 else -n) for n in frames}
         dist.barrier()
         try:
-            FrameQueue(frames, bad_cost, store)
+            FrameQueue(frames, bad_cost, store, epoch=2)   # rank / world from torch.distributed
             mismatch = False
         except RuntimeError:
             mismatch = True
@@ -168,9 +168,8 @@ def test_frame_queue_hands_out_every_frame_once(tmp_path):
         pos = [order.index(n) for n in lst]
         assert pos == sorted(pos)
     assert sorted(n for lst in r["second"] for n in lst) == list(range(5))
-    # rank 1's order is the reverse of ranks 0 and 2's: whichever stored its hash first, the
-    # queue's ranks disagree and at least one of them raised
-    assert any(r["mismatch"])
+    # rank 1's order is the reverse of ranks 0 and 2's: every rank sees the disagreement and raises
+    assert all(r["mismatch"])
 
 
 def test_frame_queue_single_process():

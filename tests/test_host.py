@@ -413,3 +413,29 @@ def test_scene_features_select_the_build(name, frame, models, build):
     else:
         got = "room" if within(_ROOM) else "mesh" if within(_MESH) else "full"
     assert got == build, "features %#x" % f
+
+
+def test_every_builder_scene_has_a_covering_build():
+    """No render can reach a case its trace-kernel build compiled out (dt_kernels.hip DT_NEED:
+    __builtin_unreachable()): for every scene the builders produce -- buildFinal(n*8) for all 300
+    frames n of `final n` / C5, with and without the OBJ models, and the dtrender modes' scenes
+    (spheres, dof, hw4, prismcyl 0..7) -- at 1, 4, 16, 64 and 256 spp (the 4- and 5-wave builds),
+    the build dt_render would launch (dt_trace_build, the same choose_build as the render) covers the
+    scene's features. dt_render also refuses a scene outside its build's mask (DT_E_INVALID)."""
+    cases = [("final", n * 8, 0) for n in range(300)] + [("final", n * 8, 1) for n in range(0, 300, 20)]
+    cases += [("spheres", 0, 0), ("dof", 0, 0), ("hw4", 0, 0)] + [("prismcyl", f, 0) for f in range(8)]
+    seen = set()
+    for name, frame, models in cases:
+        g = dt.globals_default()
+        g.use_model = models
+        built = dt.build_scene(name, frame, g)
+        for spp in (1, 4, 16, 64, 256):
+            g.antialias_samples = spp
+            kernel, sf, bf = dt.trace_build(built, g, frame)
+            assert sf & ~bf == 0, "%s(%d) models=%d spp=%d: %s covers %#x, scene %#x" % (
+                name, frame, models, spp, kernel, bf, sf)
+            seen.add(kernel)
+    # the feature builds are the ones these scenes take (DESIGN.md §4)
+    assert {"dt_trace_kernel", "dt_trace_kernel_w5", "dt_trace_kernel_mesh", "dt_trace_kernel_w5_mesh",
+            "dt_trace_kernel_tunnel", "dt_trace_kernel_w5_tunnel", "dt_trace_kernel_full",
+            "dt_trace_kernel_rpc"} <= seen, seen

@@ -88,7 +88,7 @@ def main():
     frames = parse_range(args.frames)
     if args.split == "frames":
         store = dist.distributed_c10d._get_default_store() if distributed and world > 1 else None
-        mine = iter(FrameQueue(frames, frame_costs(), store))
+        mine = iter(FrameQueue(frames, frame_costs(), store, epoch=0, rank=rank, world=world))
     elif args.split == "static":
         mine = iter([n for n in frames if n % world == rank])
     else:

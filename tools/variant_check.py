@@ -40,7 +40,16 @@ def render_all(out):
         scene.close()
         res[name] = o.cpu().numpy()
         res[name + "_rays"] = np.array([st.rays, st.shadow_rays], dtype=np.int64)
-        print("%s: %.2f ms, rays %d shadow %d" % (name, st.trace_kernel_ms, st.rays, st.shadow_rays), flush=True)
+        print("%s: %.2f ms, rays %d shadow %d, donate_overflow %d" % (
+            name, st.trace_kernel_ms, st.rays, st.shadow_rays, st.donate_overflow), flush=True)
+    # renderImageCloud (dt_sky_kernel: one cloudColor per lane, 256-thread blocks)
+    for frame in (1, 2):
+        g = dt.globals_default()
+        g.xRes, g.yRes = 640, 480
+        o = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
+        dt.render_sky(g, frame, o, dt.tiles())
+        res["sky_640_f%d" % frame] = o.cpu().numpy()
+        print("sky_640_f%d done" % frame, flush=True)
     np.savez(out, **res)
 
 
