@@ -75,6 +75,8 @@ struct HScene {
   void* dn_pool;
   uint32_t* again_list;
   unsigned int* again_n;
+  const void* sub_nodes;      // shadow-grid block subtrees
+  const uint32_t* sub_blocks;
 };
 
 #define DT_N_STAMPS (64 + 3 * 8 * 256)   // diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters):
@@ -163,6 +165,8 @@ struct dt_scene {
   ShadowGrid sg;
   void* d_sg_cells = nullptr;
   void* d_sg_list = nullptr;
+  void* d_sub_nodes = nullptr;    // shadow-grid block subtrees (ShadowGrid::sub_*)
+  void* d_sub_blocks = nullptr;
   int ftree_mode = 0;
   int boxes_ordered = 0;   // lb <= ub on every axis of every node (both trees), no NaN bound
   void* d_leaf = nullptr;
@@ -356,7 +360,7 @@ int dt_scene_prepare(const dt_scene_desc* desc, const dt_globals* g, dt_scene** 
 static void release_device(dt_scene* s)
 {
   void** bufs[] = {&s->d_pl_cells, &s->d_pl_list, &s->d_nodes, &s->d_fnodes, &s->d_bnodes, &s->d_bparent,
-                   &s->d_sg_cells, &s->d_sg_list, &s->d_leaf, &s->d_hdr, &s->d_geom, &s->d_mat, &s->d_lights,
+                   &s->d_sg_cells, &s->d_sg_list, &s->d_sub_nodes, &s->d_sub_blocks, &s->d_leaf, &s->d_hdr, &s->d_geom, &s->d_mat, &s->d_lights,
                    &s->d_tex, &s->d_zs, (void**)&s->d_stats, &s->d_launch, (void**)&s->d_sky_miss, &s->d_dn_pool,
                    (void**)&s->d_again, &s->d_launch2, (void**)&s->d_stats2};
   for (void** b : bufs) {
@@ -391,6 +395,7 @@ static int scene_upload(dt_scene* s)
   const Accel& acc = s->acc;
   int rc;
   if ((rc = upload(s->sg.cells, &s->d_sg_cells)) || (rc = upload(s->sg.list, &s->d_sg_list)) ||
+      (rc = upload(s->sg.sub_nodes, &s->d_sub_nodes)) || (rc = upload(s->sg.sub_blocks, &s->d_sub_blocks)) ||
       (rc = upload(acc.dnodes, &s->d_nodes)) || (rc = upload(acc.fnodes, &s->d_fnodes)) ||
       (rc = upload(acc.bnodes, &s->d_bnodes)) || (rc = upload(acc.bparent, &s->d_bparent)) || (rc = upload(acc.leaf, &s->d_leaf)) || (rc = upload(f.hdr, &s->d_hdr)) ||
       (rc = upload(f.geom, &s->d_geom)) || (rc = upload(f.mat, &s->d_mat)) || (rc = upload(f.lights, &s->d_lights)) ||
@@ -587,6 +592,11 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
     P.sg_base0[l] = sc->sg.base0[l];
   }
   P.sg_reach = sc->sg.reach;
+  for (int l = 0; l < DT_MAX_SGRID; ++l) P.sgb_base[l] = sc->sg.sub_base[l];
+  P.sgb_bx = sc->sg.sub_bx;
+  P.sgb_by = sc->sg.sub_by;
+  P.sgb_nbx = sc->sg.sub_nbx;
+  P.sgb_nby = sc->sg.sub_nby;
   P.sg_ypad = (float)sc->sg.ypad;
 
   P.n_lights = (int32_t)sc->flat.lights.size();
@@ -688,6 +698,8 @@ static void fill_hscene(const dt_scene* sc, HScene& hs)
   hs.tex = (const uint8_t*)sc->d_tex;
   hs.pl_cells = (const uint32_t*)sc->d_pl_cells;
   hs.pl_list = (const uint32_t*)sc->d_pl_list;
+  hs.sub_nodes = sc->d_sub_nodes;
+  hs.sub_blocks = (const uint32_t*)sc->d_sub_blocks;
 }
 
 // The trace-kernel builds (dt_kernels.hip DT_TRACE_KERNEL, Makefile TRACE_BUILDS) and the choice

@@ -197,6 +197,8 @@ struct DScene {
   void* dn_pool;            // P.donate: DT_DN_POOL_REC records of 32 B per resident wave (DFS work sharing)
   uint32_t* again_list;     // P.sky_again: the items a launch without the sky left to a launch with it
   unsigned int* again_n;    // ... and their count
+  const DNodeDev* sub_nodes;   // shadow-grid block subtrees (host_shadowgrid.cpp; P.sgb_*)
+  const uint32_t* sub_blocks;  // (first node, node count) per (light, block); count 0: none
 };
 
 // pow(x, n) for the integer exponents the reference writes as pow(x, 2.0) etc. pow(x, 1) is x
@@ -1695,14 +1697,16 @@ __device__ __forceinline__ float shadow_tcull(float t_max)
 
 // any-hit shadow test (cpp:806-855): box test with sray from isectP+sray*1e-3, shape test
 // with normalized sray from isectP+sn*1e-3, skipping the light's own shape.
+// MODE 3: a shadow-grid block subtree (sub, n_sub: host_shadowgrid.cpp), finite rays, no bump
 template <int MODE, class CNT>
 __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P, const Walk& w, bool active, V3 bstart,
-                                              V3 sn, V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
+                                              V3 sn, V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt,
+                                              const DNodeDev* sub = nullptr, int n_sub = 0)
 {
-  constexpr bool GENERAL = MODE == 1, BUMP = MODE == 2;   // as closest_hit_walk
+  constexpr bool GENERAL = MODE == 1, BUMP = MODE == 2, SUB = MODE == 3;   // as closest_hit_walk
   // fast walks use the alternative tree when one was built (DT_FAST_TREE), else the reference's
-  const bool ftree = !BUMP && !GENERAL && P.n_fnodes > 0 && (P.ftree_mode & 2);
-  const DNodeDev* const NODES = BUMP ? S.bnodes : ftree ? S.fnodes : S.nodes;   // any-hit: order free
+  const bool ftree = !BUMP && !GENERAL && !SUB && P.n_fnodes > 0 && (P.ftree_mode & 2);
+  const DNodeDev* const NODES = SUB ? sub : BUMP ? S.bnodes : ftree ? S.fnodes : S.nodes;   // any-hit: order free
   int resume = active ? 0 : 0x7fffffff;
   const unsigned long long am = __ballot(active);
   unsigned long long om = 0;   // occluded lanes
@@ -1711,7 +1715,7 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
 #ifdef DT_STAMPS
   unsigned long long nv = 0;
 #endif
-  const int n_nodes = BUMP ? P.n_bnodes : ftree ? P.n_fnodes : P.n_nodes;
+  const int n_nodes = SUB ? n_sub : BUMP ? P.n_bnodes : ftree ? P.n_fnodes : P.n_nodes;
   while (i < n_nodes) {
     const DNodeDev nd = cas(NODES)[i];
     const bool act = GENERAL ? resume <= i : inv(am & ~om);   // see closest_hit_walk
@@ -1935,6 +1939,28 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
         return bump_list ? occluded_union<true>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt)
                          : occluded_union<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
       }
+#if DT_HAS(DT_SHAPE_TRIANGLE)
+      // Some lane's cell walks the tree (a list over the cap: mesh cells). When every active lane
+      // lies in one block that has a subtree (host_shadowgrid.cpp, DT_SG_SUBTREE; pass-0 waves),
+      // the wave walks that subtree: it holds every leaf that can occlude a segment from the block.
+      if (!w.bump_wave && P.sgb_base[li] >= 0) {
+        const bool gin = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.sg_dim[0] &&
+                         fy < (float)P.sg_dim[1] && fz < (float)P.sg_dim[2];
+        const int blk = gin ? ((int)fz * P.sgb_nby + (int)fy / P.sgb_by) * P.sgb_nbx + (int)fx / P.sgb_bx : -1;
+        const int b0 = __builtin_amdgcn_readlane(blk, (int)__builtin_ctzll(__ballot(active)));
+        if (b0 >= 0 && !__ballot(active && blk != b0)) {
+          const uint2 e = ((const uint2*)S.sub_blocks)[(size_t)P.sgb_base[li] + b0];
+          if (e.y > 0) {
+            DT_CNT(63);
+#ifdef DT_STAMPS
+            cnt.cur_path = 3;
+#endif
+            return occluded_walk<3>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, cnt,
+                                    S.sub_nodes + uni((int)e.x), uni((int)e.y));
+          }
+        }
+      }
+#endif
     }
   }
 #ifdef DT_STAMPS

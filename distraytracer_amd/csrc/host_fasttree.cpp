@@ -190,6 +190,29 @@ bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNo
   return true;
 }
 
+void build_fast_subtree(const std::vector<dtd::DNodeDev>& ref, const std::vector<int32_t>& leaf_nodes,
+                        std::vector<dtd::DNodeDev>& out)
+{
+  out.clear();
+  Builder b(ref, 0.0, nullptr);
+  for (int32_t i : leaf_nodes) {
+    LeafRef L;
+    for (int a = 0; a < 3; ++a) {
+      L.lb[a] = ref[i].lb[a];
+      L.ub[a] = ref[i].ub[a];
+      L.c[a] = 0.5 * (L.lb[a] + L.ub[a]);
+    }
+    L.node = i;
+    L.rank = (int)b.leaves.size();   // any-hit walks: the order of the leaves does not matter
+    b.leaves.push_back(L);
+  }
+  if (b.leaves.empty()) return;
+  std::vector<int> ids(b.leaves.size());
+  for (size_t i = 0; i < ids.size(); ++i) ids[i] = (int)i;
+  b.build(ids, 0, (int)ids.size());
+  out.swap(b.out);
+}
+
 std::vector<int32_t> tree_parents(const std::vector<dtd::DNodeDev>& ref)
 {
   // pre-order with skip = end of the subtree for inner nodes (a leaf's subtree ends at i + 1)

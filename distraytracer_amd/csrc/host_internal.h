@@ -28,11 +28,16 @@ void build_bvh(const dt_scene_desc& d, const dt_globals& g, FlatBVH& out);
 // can reach (host_fasttree.cpp) instead of +-ypad
 bool build_fast_tree(const std::vector<dtd::DNodeDev>& ref, std::vector<dtd::DNodeDev>& out, double ypad = 0,
                      const double* eye = nullptr, bool up_only = false);
+// the same SAH tree over a subset of the reference's leaves (node indices into ref), for the shadow
+// grid's block subtrees: leaves are copies of the reference leaves (skip links local to `out`)
+void build_fast_subtree(const std::vector<dtd::DNodeDev>& ref, const std::vector<int32_t>& leaf_nodes,
+                        std::vector<dtd::DNodeDev>& out);
 // parent of every node of a pre-order skip-link tree (-1 at the root)
 std::vector<int32_t> tree_parents(const std::vector<dtd::DNodeDev>& ref);
 
 // host_shadowgrid.cpp: per-light candidate-occluder lists per grid cell (false: no grid)
 struct ShadowGrid {
+  ShadowGrid() { for (int l = 0; l < DT_MAX_SGRID; ++l) sub_base[l] = -1; }
   int n_lights = 0;                  // lights 0..n_lights-1 (base[l] < 0: that light has none)
   int32_t base[DT_MAX_SGRID] = {};   // first cell record of light l in `cells`
   int32_t base0[DT_MAX_SGRID] = {};  // the same for pass-0 (unshifted) rays: `base`, or an unpadded
@@ -43,6 +48,14 @@ struct ShadowGrid {
   std::vector<uint32_t> cells;       // (offset into list | DT_SG_UMBRA, count | DT_SG_WALK) per cell
   std::vector<int32_t> list;         // leaf node indices (reference tree)
   double ypad = 0;                   // lists also hold for blur passes with |shift| <= ypad
+  // Block subtrees (DT_SG_SUBTREE): for each block of sub_bx x sub_by x 1 cells holding a cell that
+  // walks the tree, an SAH tree over the leaves whose box meets the block's swept box to the light
+  // (the block's list, uncapped). Pass-0 waves whose lanes all lie in one such block walk it instead
+  // of the whole tree (C4's mesh cells).
+  int sub_bx = 0, sub_by = 0, sub_nbx = 0, sub_nby = 0;
+  int32_t sub_base[DT_MAX_SGRID];        // light l's first block record in sub_blocks (-1: none)
+  std::vector<uint32_t> sub_blocks;      // (first node, node count) per block; count 0: none
+  std::vector<dtd::DNodeDev> sub_nodes;
   long plane_dropped = 0;            // (leaf, cell) pairs left out by plane culling (diagnostic)
   long umbra_cells = 0;              // (light, cell) records flagged DT_SG_UMBRA (diagnostic)
 };

@@ -215,6 +215,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   const double t_entry = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
   const std::vector<dtd::DLight>& lights = fs.lights;
   g = ShadowGrid();
+  for (int l = 0; l < DT_MAX_SGRID; ++l) g.sub_base[l] = -1;
   g.reach = reach;
   g.ypad = ypad;
   if (nodes.empty() || !(nodes[0].lb[0] <= nodes[0].ub[0])) return false;
@@ -773,6 +774,101 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   if (timing)
     fprintf(stderr, "  shadow grid: tests and umbra of %zu lights %.2f ms (%d threads), lists %.2f ms\n", nl,
             t_tests - t_setup, std::max(1, std::min(hw_threads, 16)), now_ms() - t_tests);
+  // Block subtrees (ShadowGrid::sub_*; DT_SG_SUBTREE=1; for pass-0 rays, whose leaf boxes are the
+  // reference's: lists selected with blur-padded boxes only hold more leaves than they need). A cell
+  // whose list exceeds the cap walks the whole tree; for the blocks of BX x BY x 1 cells that hold
+  // such a cell, the leaves whose box meets the block's swept box to the light (every segment from
+  // any cell of the block, reach margin m1 included, lies in it) and whose shapes are not all
+  // plane-separated from it, under SAH inner nodes. The device walks it for pass-0 waves whose
+  // active lanes all lie in the block: every leaf that can hold an occluder of their segments is
+  // in it, the walk's box tests and shape tests are the full tree's, and any-hit order is free.
+  const char* sst = getenv("DT_SG_SUBTREE");
+  if (sst && sst[0] == '1') {
+    const double t_sub = now_ms();
+    // DT_SG_SUB_BLOCK: the subtree blocks' size in cells (XxY, default the grid tests' 8x4): smaller
+    // blocks hold shorter lists, larger ones serve more scattered waves
+    int SBX = std::max(1, blk_x), SBY = std::max(1, blk_y);
+    if (getenv("DT_SG_SUB_BLOCK") && !sg_parse_block(getenv("DT_SG_SUB_BLOCK"), SBX, SBY))
+      fprintf(stderr, "dt: DT_SG_SUB_BLOCK='%s' not understood (use XxY): 8x4\n", getenv("DT_SG_SUB_BLOCK"));
+    SBX = std::max(1, SBX);
+    SBY = std::max(1, SBY);
+    g.sub_bx = SBX;
+    g.sub_by = SBY;
+    g.sub_nbx = (g.dim[0] + SBX - 1) / SBX;
+    g.sub_nby = (g.dim[1] + SBY - 1) / SBY;
+    const size_t nblk = (size_t)g.sub_nbx * g.sub_nby * g.dim[2];
+    struct SubItem { int l; size_t blk; };
+    std::vector<SubItem> sitems;
+    for (size_t l = 0; l < (size_t)DT_MAX_SGRID; ++l) g.sub_base[l] = -1;
+    for (size_t l = 0; l < nl; ++l) {
+      if (!ls[l].on || g.base[l] < 0) continue;
+      std::vector<char> mark(nblk, 0);
+      bool any = false;
+      for (int c = 0; c < ncell; ++c)
+        if (g.cells[2 * ((size_t)g.base[l] + c) + 1] == DT_SG_WALK) {
+          const int x = c % g.dim[0], y = (c / g.dim[0]) % g.dim[1], z = c / (g.dim[0] * g.dim[1]);
+          mark[((size_t)z * g.sub_nby + y / SBY) * g.sub_nbx + x / SBX] = 1;
+          any = true;
+        }
+      if (!any) continue;
+      g.sub_base[l] = (int32_t)(g.sub_blocks.size() / 2);
+      g.sub_blocks.resize(g.sub_blocks.size() + 2 * nblk, 0u);
+      for (size_t k = 0; k < nblk; ++k)
+        if (mark[k]) sitems.push_back({(int)l, k});
+    }
+    std::vector<std::vector<dtd::DNodeDev>> sub(sitems.size());
+    std::atomic<size_t> next(0);
+    auto runner = [&]() {
+      std::vector<int> shp;
+      std::vector<int32_t> list;
+      for (size_t k; (k = next.fetch_add(1)) < sitems.size();) {
+        const size_t l = (size_t)sitems[k].l, blk = sitems[k].blk;
+        const LightSetup& S = ls[l];
+        const dtd::DLight& L = lights[l];
+        const int z = (int)(blk / ((size_t)g.sub_nbx * g.sub_nby));
+        const int by = (int)((blk / g.sub_nbx) % g.sub_nby), bx = (int)(blk % g.sub_nbx);
+        const int c0[3] = {bx * SBX, by * SBY, z};
+        const int c1[3] = {std::min((bx + 1) * SBX, g.dim[0]) - 1, std::min((by + 1) * SBY, g.dim[1]) - 1, z};
+        double clo[3], chi[3];
+        for (int a = 0; a < 3; ++a) {
+          clo[a] = lo[a] + c0[a] * hh[a] - m1;
+          chi[a] = lo[a] + (c1[a] + 1) * hh[a] + m1;
+        }
+        list.clear();
+        for (int leaf : leaves) {
+          const dtd::DNodeDev& nd = nodes[leaf];
+          if ((nd.meta & dtd::DN_SINGLE) && (int32_t)nd.first == L.shape_index) continue;   // cpp:832
+          if (!swept_meets(clo, chi, S.llo, S.lhi, lbox[leaf].data(), lbox[leaf].data() + 3)) continue;
+          leaf_shapes(leaf, shp);
+          bool sep = !shp.empty();
+          for (int sid : shp)
+            if (sid != L.shape_index &&
+                !shape_separated(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, clo, chi, S.llo, S.lhi, mplane, ypad)) {
+              sep = false;
+              break;
+            }
+          if (!sep) list.push_back(leaf);
+        }
+        build_fast_subtree(nodes, list, sub[k]);
+      }
+    };
+    {
+      const int np = std::max(1, std::min(hw_threads, 16));
+      std::vector<std::thread> pool;
+      for (int t = 1; t < np; ++t) pool.emplace_back(runner);
+      runner();
+      for (auto& th : pool) th.join();
+    }
+    for (size_t k = 0; k < sitems.size(); ++k) {
+      const size_t rec = (size_t)g.sub_base[sitems[k].l] + sitems[k].blk;
+      g.sub_blocks[2 * rec] = (uint32_t)g.sub_nodes.size();
+      g.sub_blocks[2 * rec + 1] = (uint32_t)sub[k].size();
+      g.sub_nodes.insert(g.sub_nodes.end(), sub[k].begin(), sub[k].end());
+    }
+    if (timing)
+      fprintf(stderr, "  shadow grid: %zu block subtrees, %zu nodes, %.2f ms\n", sitems.size(), g.sub_nodes.size(),
+              now_ms() - t_sub);
+  }
   g.plane_dropped = dropped;
   if (timing) fprintf(stderr, "  shadow grid lights: %.2f ms\n", now_ms() - t_setup);
   return g.n_lights > 0;

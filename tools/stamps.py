@@ -50,8 +50,9 @@ def main():
     print("shadow grid per item: list tests %.1f, list walks %.2f, cell lookups inside %.2f / outside %.2f, "
           "list too long %.2f" % (arr[34] / items, arr[35] / items, arr[36] / items, arr[38] / items, arr[37] / items))
     print("scattered shadow waves per item %.2f, union walks %.2f" % (arr[40] / items, arr[41] / items))
-    print("wave-level shadow prim tests per item by path: cell list %.2f, union %.2f, tree walk %.2f"
-          % (arr[42] / items, arr[43] / items, arr[44] / items))
+    print("wave-level shadow prim tests per item by path: cell list %.2f, union %.2f, tree walk %.2f, "
+          "block subtree %.2f" % (arr[42] / items, arr[43] / items, arr[44] / items, arr[45] / items))
+    print("block-subtree shadow walks per item %.2f (DT_SG_SUBTREE=1)" % (arr[63] / items))
     print("shadow walks per item: all occluded %.2f (%.1f visits/walk), none occluded %.2f (%.1f/walk), total %.2f"
           % (arr[29] / items, arr[28] / max(arr[29], 1), arr[31] / items, arr[30] / max(arr[31], 1), arr[9] / items))
     # per (light, shape) shadow tests: wave-level tests per item, lanes per test, lane hit fraction
