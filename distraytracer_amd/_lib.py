@@ -104,7 +104,8 @@ class AccelInfo(ctypes.Structure):
                 ("sg_list_pool", c_int64), ("sg_list_entries", c_int64), ("nodes_hash", c_uint64),
                 ("fnodes_hash", c_uint64), ("bnodes_hash", c_uint64), ("sg_hash", c_uint64),
                 ("sg_contents_hash", c_uint64), ("bump_pad", c_float), ("sg_reach", c_float),
-                ("sg_umbra_cells", c_int64), ("features", ctypes.c_uint32)]
+                ("sg_umbra_cells", c_int64), ("features", ctypes.c_uint32),
+                ("sg_sub_blocks", c_int32), ("sg_sub_nodes", c_int64), ("sg_sub_hash", c_uint64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}

@@ -528,6 +528,14 @@ int dt_accel_info_build(const dt_scene_desc* desc, const dt_globals* g, dt_accel
   info->n_bnodes = a.n_bnodes;
   info->boxes_ordered = a.boxes_ordered;
   info->features = scene_features(*desc);
+  for (size_t b = 1; b < a.sg.sub_blocks.size(); b += 2) info->sg_sub_blocks += a.sg.sub_blocks[b] > 0;
+  info->sg_sub_nodes = (int64_t)a.sg.sub_nodes.size();
+  {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
+    for (uint32_t x : a.sg.sub_blocks) mix(x);
+    info->sg_sub_hash = (h ^ nodes_hash(a.sg.sub_nodes)) * 1099511628211ull;
+  }
   info->sg_lights = a.sg.n_lights;
   for (int k = 0; k < 3; ++k) info->sg_dim[k] = a.sg.dim[k];
   info->sg_cells = (int64_t)(a.sg.cells.size() / 2);

@@ -309,6 +309,9 @@ typedef struct dt_accel_info {
   uint32_t features;           /* the scene's trace-kernel feature mask: bit t for shape type t,
                                   12 sphere lights/emitters, 13 Oren-Nayar, 14 glass, 15 rectangle
                                   lights/emitters (the build dt_render launches) */
+  int32_t sg_sub_blocks;       /* shadow-grid block subtrees (DT_SG_SUBTREE=1) and their nodes */
+  int64_t sg_sub_nodes;
+  uint64_t sg_sub_hash;        /* FNV-1a over the block records and subtree nodes */
 } dt_accel_info;
 int dt_accel_info_build(const dt_scene_desc* desc, const dt_globals* g, dt_accel_info* info);
 

@@ -439,3 +439,25 @@ def test_every_builder_scene_has_a_covering_build():
     assert {"dt_trace_kernel", "dt_trace_kernel_w5", "dt_trace_kernel_mesh", "dt_trace_kernel_w5_mesh",
             "dt_trace_kernel_tunnel", "dt_trace_kernel_w5_tunnel", "dt_trace_kernel_full",
             "dt_trace_kernel_rpc"} <= seen, seen
+
+
+def test_block_subtrees_host_build(monkeypatch):
+    """DT_SG_SUBTREE=1 (host_shadowgrid.cpp): C4's mesh cells walk the tree (lists over the cap), so
+    their blocks get subtrees; the build is deterministic (thread pool, same hash twice) and off by
+    default; smaller blocks give more, smaller subtrees."""
+    g = dt.globals_default()
+    g.use_model = 1
+    built = dt.build_scene("final", 240, g)
+    g.xRes, g.yRes, g.antialias_samples = 1920, 1080, 256
+    monkeypatch.delenv("DT_SG_SUBTREE", raising=False)
+    monkeypatch.delenv("DT_SG_SUB_BLOCK", raising=False)
+    off = dt.accel_info(built, g)
+    assert off["sg_tree_cells"] > 0 and off["sg_sub_blocks"] == 0 and off["sg_sub_nodes"] == 0
+    monkeypatch.setenv("DT_SG_SUBTREE", "1")
+    a, b = dt.accel_info(built, g), dt.accel_info(built, g)
+    assert a["sg_sub_blocks"] > 0 and a["sg_sub_nodes"] >= a["sg_sub_blocks"]
+    assert a["sg_sub_hash"] == b["sg_sub_hash"]
+    assert a["sg_hash"] == off["sg_hash"]   # the cells and lists themselves are unchanged
+    monkeypatch.setenv("DT_SG_SUB_BLOCK", "4x2")
+    c = dt.accel_info(built, g)
+    assert c["sg_sub_blocks"] > a["sg_sub_blocks"]
