@@ -605,6 +605,10 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   P.sgb_by = sc->sg.sub_by;
   P.sgb_nbx = sc->sg.sub_nbx;
   P.sgb_nby = sc->sg.sub_nby;
+  // DT_SG_SUB_MULTI: a wave whose lanes lie in up to this many blocks walks their subtrees in turn
+  // (default 1: only waves within one block); read per render
+  const char* smu = getenv("DT_SG_SUB_MULTI");
+  P.sgb_multi = smu && atoi(smu) > 0 ? atoi(smu) : 1;
   P.sg_ypad = (float)sc->sg.ypad;
 
   P.n_lights = (int32_t)sc->flat.lights.size();

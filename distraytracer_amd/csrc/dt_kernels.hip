@@ -1943,21 +1943,39 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       // Some lane's cell walks the tree (a list over the cap: mesh cells). When every active lane
       // lies in one block that has a subtree (host_shadowgrid.cpp, DT_SG_SUBTREE; pass-0 waves),
       // the wave walks that subtree: it holds every leaf that can occlude a segment from the block.
+      // Lanes in up to P.sgb_multi blocks (DT_SG_SUB_MULTI) walk their blocks' subtrees one after
+      // another, each with its own lanes; otherwise the whole tree as before.
       if (!w.bump_wave && P.sgb_base[li] >= 0) {
         const bool gin = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.sg_dim[0] &&
                          fy < (float)P.sg_dim[1] && fz < (float)P.sg_dim[2];
         const int blk = gin ? ((int)fz * P.sgb_nby + (int)fy / P.sgb_by) * P.sgb_nbx + (int)fx / P.sgb_bx : -1;
-        const int b0 = __builtin_amdgcn_readlane(blk, (int)__builtin_ctzll(__ballot(active)));
-        if (b0 >= 0 && !__ballot(active && blk != b0)) {
-          const uint2 e = ((const uint2*)S.sub_blocks)[(size_t)P.sgb_base[li] + b0];
-          if (e.y > 0) {
+        const uint2* const recs = (const uint2*)S.sub_blocks + P.sgb_base[li];
+        // the wave's distinct blocks, each with a subtree, at most sgb_multi of them
+        unsigned long long rem = __ballot(active);
+        int nb = 0;
+        while (rem && nb < P.sgb_multi) {
+          const int b0 = __builtin_amdgcn_readlane(blk, (int)__builtin_ctzll(rem));
+          if (b0 < 0 || recs[b0].y == 0) break;
+          rem &= ~__ballot(blk == b0);
+          ++nb;
+        }
+        if (!rem) {
+          bool occl = false;
+          unsigned long long todo = __ballot(active);
+          while (todo) {
+            const int b0 = __builtin_amdgcn_readlane(blk, (int)__builtin_ctzll(todo));
+            const uint2 e = recs[b0];
+            const bool mine = inv(todo) && blk == b0;
+            todo &= ~__ballot(mine);
             DT_CNT(63);
 #ifdef DT_STAMPS
             cnt.cur_path = 3;
 #endif
-            return occluded_walk<3>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, cnt,
-                                    S.sub_nodes + uni((int)e.x), uni((int)e.y));
+            const bool o = occluded_walk<3>(S, P, w, mine, bstart, sn, sstart, t_max, skip_shape, 0.0f, cnt,
+                                            S.sub_nodes + uni((int)e.x), uni((int)e.y));
+            occl = occl || (mine && o);
           }
+          return occl;
         }
       }
 #endif

@@ -192,6 +192,7 @@ struct DParams {
   // cells, sgb_nbx x sgb_nby per layer; light l's records at sgb_base[l] (-1: none)
   int32_t sgb_base[DT_MAX_SGRID];
   int32_t sgb_bx, sgb_by, sgb_nbx, sgb_nby;
+  int32_t sgb_multi;      // a wave walks the subtrees of up to this many blocks in turn (DT_SG_SUB_MULTI)
 };
 
 #ifndef DT_HD

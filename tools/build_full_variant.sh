@@ -12,5 +12,7 @@ rm -rf "$W/distraytracer_amd/csrc/build"
 cp "$R"/include/*.h "$W/include/"
 make -s -j8 -C "$W/distraytracer_amd/csrc" ../libdt.so "$@" 2>&1 | grep -v warning || true
 mkdir -p "$R/distraytracer_amd/variants"
-cp "$W/distraytracer_amd/libdt.so" "$R/distraytracer_amd/variants/libdt_$name.so"
+# copy then rename: a snapshot of the tree taken meanwhile (gpurun) never sees a half-written library
+cp "$W/distraytracer_amd/libdt.so" "$R/distraytracer_amd/variants/.libdt_$name.so.tmp"
+mv "$R/distraytracer_amd/variants/.libdt_$name.so.tmp" "$R/distraytracer_amd/variants/libdt_$name.so"
 echo "built distraytracer_amd/variants/libdt_$name.so"

@@ -28,7 +28,10 @@ def render_all(out):
     import torch
     import distraytracer_amd as dt
     res = {}
+    only = os.environ.get("VC_CASES")   # comma-separated case names (default: all)
     for name, b, frame, models, W, H, spp, depth, world in CASES:
+        if only and name not in only.split(","):
+            continue
         g = dt.globals_default()
         g.use_model = models
         built = dt.build_scene(b, frame, g)
@@ -43,7 +46,7 @@ def render_all(out):
         print("%s: %.2f ms, rays %d shadow %d, donate_overflow %d" % (
             name, st.trace_kernel_ms, st.rays, st.shadow_rays, st.donate_overflow), flush=True)
     # renderImageCloud (dt_sky_kernel: one cloudColor per lane, 256-thread blocks)
-    for frame in (1, 2):
+    for frame in ((1, 2) if not only or "sky" in only else ()):
         g = dt.globals_default()
         g.xRes, g.yRes = 640, 480
         o = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
