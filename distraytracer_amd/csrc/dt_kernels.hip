@@ -1940,28 +1940,38 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
                          : occluded_union<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
       }
 #if DT_HAS(DT_SHAPE_TRIANGLE)
-      // Some lane's cell walks the tree (a list over the cap: mesh cells). When every active lane
-      // lies in one block that has a subtree (host_shadowgrid.cpp, DT_SG_SUBTREE; pass-0 waves),
-      // the wave walks that subtree: it holds every leaf that can occlude a segment from the block.
-      // Lanes in up to P.sgb_multi blocks (DT_SG_SUB_MULTI) walk their blocks' subtrees one after
-      // another, each with its own lanes; otherwise the whole tree as before.
+      // Some lanes' cells walk the tree (lists over the cap: C4's mesh cells; with scattered glossy
+      // bounces one such lane used to send all 64 down the whole tree). With block subtrees
+      // (host_shadowgrid.cpp, DT_SG_SUBTREE; pass-0 waves, every lane inside the grid) the wave is
+      // split: the lanes of list cells take the union of their lists as above, and the lanes of
+      // tree-walk cells, when they lie in at most P.sgb_multi blocks (DT_SG_SUB_MULTI), walk their
+      // blocks' subtrees, one block after another with its own lanes. A block's subtree holds every
+      // leaf that can occlude a segment from any of its cells. Otherwise the whole tree as before.
       if (!w.bump_wave && P.sgb_base[li] >= 0) {
         const bool gin = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.sg_dim[0] &&
                          fy < (float)P.sg_dim[1] && fz < (float)P.sg_dim[2];
         const int blk = gin ? ((int)fz * P.sgb_nby + (int)fy / P.sgb_by) * P.sgb_nbx + (int)fx / P.sgb_bx : -1;
         const uint2* const recs = (const uint2*)S.sub_blocks + P.sgb_base[li];
-        // the wave's distinct blocks, each with a subtree, at most sgb_multi of them
-        unsigned long long rem = __ballot(active);
+        const bool wl = active && !lin;   // lanes in tree-walk cells (or outside the grid: blk < 0)
+        unsigned long long rem = __ballot(wl);
         int nb = 0;
         while (rem && nb < P.sgb_multi) {
           const int b0 = __builtin_amdgcn_readlane(blk, (int)__builtin_ctzll(rem));
           if (b0 < 0 || recs[b0].y == 0) break;
-          rem &= ~__ballot(blk == b0);
+          rem &= ~__ballot(wl && blk == b0);
           ++nb;
         }
         if (!rem) {
           bool occl = false;
-          unsigned long long todo = __ballot(active);
+          const bool ll = active && lin;
+          if (__ballot(ll)) {
+            DT_CNT(41);
+#ifdef DT_STAMPS
+            cnt.cur_path = 1;
+#endif
+            occl = occluded_union<false>(S, w, ll, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt) && ll;
+          }
+          unsigned long long todo = __ballot(wl);
           while (todo) {
             const int b0 = __builtin_amdgcn_readlane(blk, (int)__builtin_ctzll(todo));
             const uint2 e = recs[b0];
@@ -2877,6 +2887,60 @@ struct DLaunch {
 #ifndef DT_TRACE_MIN_WAVES
 #define DT_TRACE_MIN_WAVES 1
 #endif
+#ifndef DT_REPRO
+#define DT_REPRO 0
+#endif
+#if DT_REPRO
+// DT_REPRO=1 (tools/call_repro: never part of libdt.so): the sky of dt_sky_miss_kernel (cpp:1074-1092,
+// cloudColor of mcam * focalPoint per pixel) through cloud_color_lane inlined and through the same
+// function behind a real call, on the same pixels, for the called-function defect
+__device__ __noinline__ V3 cloud_color_lane_call(const DParams& P, const float* __restrict__ zs, V3 ray)
+{
+  return cloud_color_lane(P, zs, ray);
+}
+template <bool CALL>
+__device__ __forceinline__ void repro_sky(const DParams* __restrict__ Pp, const float* __restrict__ zs, int x0, int y0,
+                                          int w, int n, double* __restrict__ out)
+{
+  const DParams& P = *Pp;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n) {
+    const int x = x0 + q % w, y = y0 + q / w;
+    const V3 eye = v3a(P.eye), X = v3a(P.X), Y = v3a(P.Y), Z = v3a(P.Z);
+    float aa = P.l + (P.r - P.l) * (float)x / (float)P.xRes;
+    float bb = P.b + (P.t - P.b) * (float)y / (float)P.yRes;
+    V3 rd = sub(add(mul(aa, X), mul(bb, Y)), mul(P.near_plane, Z));
+    V3 fp = add(eye, mul(P.focal_length, rd));
+    V3 pt;
+    pt.x = ((P.sky_m[0][0] * fp.x + P.sky_m[0][1] * fp.y) + P.sky_m[0][2] * fp.z) + P.sky_m[0][3] * 1.0;
+    pt.y = ((P.sky_m[1][0] * fp.x + P.sky_m[1][1] * fp.y) + P.sky_m[1][2] * fp.z) + P.sky_m[1][3] * 1.0;
+    pt.z = ((P.sky_m[2][0] * fp.x + P.sky_m[2][1] * fp.y) + P.sky_m[2][2] * fp.z) + P.sky_m[2][3] * 1.0;
+    const V3 c = CALL ? cloud_color_lane_call(P, zs, pt) : cloud_color_lane(P, zs, pt);
+    out[3 * q] = c.x;
+    out[3 * q + 1] = c.y;
+    out[3 * q + 2] = c.z;
+  }
+}
+extern "C" __global__ void __launch_bounds__(256) dt_repro_inline(const DParams* Pp, const float* zs, int x0, int y0,
+                                                                  int w, int n, double* out)
+{
+  repro_sky<false>(Pp, zs, x0, y0, w, n, out);
+}
+extern "C" __global__ void __launch_bounds__(256) dt_repro_call(const DParams* Pp, const float* zs, int x0, int y0,
+                                                                int w, int n, double* out)
+{
+  repro_sky<true>(Pp, zs, x0, y0, w, n, out);
+}
+extern "C" hipError_t dt_repro_launch(int call, const void* Pp, const float* zs, int x0, int y0, int w, int n,
+                                      double* out)
+{
+  if (call)
+    hipLaunchKernelGGL(dt_repro_call, dim3((n + 255) / 256), dim3(256), 0, 0, (const DParams*)Pp, zs, x0, y0, w, n, out);
+  else
+    hipLaunchKernelGGL(dt_repro_inline, dim3((n + 255) / 256), dim3(256), 0, 0, (const DParams*)Pp, zs, x0, y0, w, n, out);
+  return hipGetLastError();
+}
+#else   // !DT_REPRO
 #if DT_ISECT
 // Intersection micro-benchmark (2^24 primary rays of the C3 camera): rayColor's first
 // step for the camera's primary rays (getDOFSamples + getPerspEyeRay, cpp:195-210 / 1044-1072; the
@@ -3384,3 +3448,4 @@ extern "C" int DT_CAT(DT_TRACE_KERNEL, _traits)(void)
   return (DT_SKY_AGAIN ? 1 : 0) | (int)(((DT_FEATURES) & 0xFFFFu) << 8);
 }
 #endif
+#endif   // !DT_REPRO
