@@ -400,35 +400,23 @@ __device__ V3 cloud_finish(const DParams& P, V3 color)
 #define DT_CLOUD_ABOVE 1.3126
 #define DT_CLOUD_BELOW (-2.3126)
 
-// DT_SKY_CALL=1 (diagnostic builds only, tools/call_repro): the two cloudColor entry points below
-// emitted as real calls instead of inlined, to study the called-march defect
+// DT_SKY_CALL=1: the two cloudColor entry points below emitted as real calls instead of inlined
+// (csrc/Makefile: the tunnel and blur builds, whose cooperative march would otherwise shape the
+// trace kernel's register allocation: VGPR spills 158 -> 71 in the 5-wave blur build). The called
+// march used to return wrong colours: the cause was -mllvm -disable-machine-cse, no longer among
+// the code-generation flags (tools/call_repro, tests/test_codegen.py).
 #ifndef DT_SKY_CALL
 #define DT_SKY_CALL 0
 #endif
 #if DT_SKY_CALL
 #define DT_SKY_FN __noinline__
-// the callee checks its workitem id (threadIdx.x, an implicit input of a call) against the lane id
-// from v_mbcnt (no input): mismatches are counted in dt_stats.donate_overflow (unused outside the
-// work-sharing build). DT_SKY_CALL=2 takes the cooperative march's lane from v_mbcnt.
-#define DT_SKY_DBG , unsigned long long* __restrict__ dbg
-#define DT_SKY_DBG_ARG(p) , (p)
-#define DT_SKY_TID_CHECK() do { if ((int)(threadIdx.x & 63) != (int)__lane_id()) atomicAdd(dbg, 1ull); } while (0)
 #else
 #define DT_SKY_FN __forceinline__
-#define DT_SKY_DBG
-#define DT_SKY_DBG_ARG(p)
-#define DT_SKY_TID_CHECK() do { } while (0)
-#endif
-#if DT_SKY_CALL == 2
-#define DT_SKY_LANE() ((int)__lane_id())
-#else
-#define DT_SKY_LANE() ((int)(threadIdx.x & 63))
 #endif
 
 // full cloudColor on one lane
-__device__ DT_SKY_FN V3 cloud_color_lane(const DParams& P, const float* __restrict__ zs, V3 ray DT_SKY_DBG)
+__device__ DT_SKY_FN V3 cloud_color_lane(const DParams& P, const float* __restrict__ zs, V3 ray)
 {
-  DT_SKY_TID_CHECK();
   V3 sky = sky_color(P, ray);
   V3 color = sky;
   for (int s = 0; s < P.n_cloud_steps; ++s) {
@@ -449,12 +437,11 @@ __device__ DT_SKY_FN V3 cloud_color_lane(const DParams& P, const float* __restri
 // spread over lanes (the noise is 99% of the work), the per-channel recurrence then runs
 // on lanes 0..2 in step order, so every addition happens in the reference's order.
 __device__ DT_SKY_FN V3 cloud_color_coop(const DParams& P, const float* __restrict__ zs, V3 ray,
-                               float* __restrict__ dens, double* __restrict__ chan DT_SKY_DBG)
+                               float* __restrict__ dens, double* __restrict__ chan)
 {
   // the march in chunks of DT_CLOUD_CHUNK steps: densities in parallel over the lanes, then
   // the per-channel recurrence on lanes 0-2 in step order (same arithmetic as one pass)
-  DT_SKY_TID_CHECK();
-  const int lane = DT_SKY_LANE();
+  const int lane = (int)(threadIdx.x & 63);
   V3 sky = sky_color(P, ray);
   double c = lane == 0 ? sky.x : (lane == 1 ? sky.y : sky.z);
   const double rev = lane == 0 ? sky.z : (lane == 1 ? sky.y : sky.x);
@@ -1897,7 +1884,7 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
     const float r = P.sg_reach;
     const bool near = (x >= x0 - r) & (x <= x0 + 1.0f + r) & (y >= y0 - r) & (y <= y0 + 1.0f + r) &
                       (z >= z0 - r) & (z <= z0 + 1.0f + r);
-    DT_CNT(inside ? 36 : 38);
+    DT_CNT(inside ? 36 : 38);   // (stamps: 38 is 0 in every config measured; also counts scattered waves below)
     if (inside && !__ballot(active & !near)) {
       const int c0 = ((int)z0 * P.sg_dim[1] + (int)y0) * P.sg_dim[0] + (int)x0;
       const DT_CAS uint32_t* e = cas(S.sg_cells) + 2 * (size_t)(sg_b + c0);
@@ -1931,6 +1918,11 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       // (a wave with some lanes outside the lists walks the tree for all of them: splitting it,
       // the union for the others, measured C3 +0.9% and C4 -3.2%, profiles/r03t)
       const unsigned long long out_lanes = __ballot(active && !lin);
+#ifdef DT_STAMPS
+      if (out_lanes && __ballot(active && !(fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.sg_dim[0] &&
+                                            fy < (float)P.sg_dim[1] && fz < (float)P.sg_dim[2])))
+        cnt.ph[38] += 1;   // a scattered wave with a lane outside the grid
+#endif
       if (!out_lanes) {
         DT_CNT(41);
 #ifdef DT_STAMPS
@@ -3103,7 +3095,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     bool px_valid = false;
     pixel_of(P, item * group + (j < group ? j : 0), px_x, px_y, px_off, px_valid);
 #ifdef DT_ITEM_TIMES
-    const unsigned long long item_t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long item_t0 = DT_ITEM_TIMES == 2 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
 #endif
 
     for (int chunk = 0; chunk < P.chunks; ++chunk) {
@@ -3186,7 +3178,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
             pt.x = ((P.sky_m[0][0] * fp.x + P.sky_m[0][1] * fp.y) + P.sky_m[0][2] * fp.z) + P.sky_m[0][3] * 1.0;
             pt.y = ((P.sky_m[1][0] * fp.x + P.sky_m[1][1] * fp.y) + P.sky_m[1][2] * fp.z) + P.sky_m[1][3] * 1.0;
             pt.z = ((P.sky_m[2][0] * fp.x + P.sky_m[2][1] * fp.y) + P.sky_m[2][2] * fp.z) + P.sky_m[2][3] * 1.0;
-            V3 skyc = cloud_color_coop(P, S.cloud_z, pt, dens, chan DT_SKY_DBG_ARG(S.stats + ST_DN_OVF));
+            V3 skyc = cloud_color_coop(P, S.cloud_z, pt, dens, chan);
             if (miss && j == jj) tmp_color = skyc;
             if (lane == 0) sky_px++;
           }
@@ -3233,9 +3225,16 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         V3 color = divs(v3(psum[0][lane], psum[1][lane], psum[2][lane]), spp);
 #ifdef DT_ITEM_TIMES   // diagnostic builds (tools/item_times.py): the item's wave cycles / 1e4, raw
         {
-          const float cyc = (float)(__builtin_amdgcn_s_memtime() - item_t0) * 1e-4f;
           const int64_t off = P.layout == DT_OUT_SLAB ? qo : 3 * ((int64_t)(P.yRes - 1 - qy) * P.xRes + qx);
+#if DT_ITEM_TIMES == 2   // tools/tail.py: start and end on the 100 MHz clock, 24-bit pieces (exact in f32)
+          const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+          out[off] = (float)(uint32_t)(item_t0 & 0xFFFFFF);
+          out[off + 1] = (float)(uint32_t)(t1 & 0xFFFFFF);
+          out[off + 2] = (float)(uint32_t)((t1 >> 24) & 0xFFFFFF);
+#else
+          const float cyc = (float)(__builtin_amdgcn_s_memtime() - item_t0) * 1e-4f;
           out[off] = cyc; out[off + 1] = cyc; out[off + 2] = cyc;
+#endif
         }
 #else
         store_pixel(P, out, qx, qy, qo, color);
@@ -3317,7 +3316,7 @@ dt_sky_miss_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     pt.x = ((P.sky_m[0][0] * fp.x + P.sky_m[0][1] * fp.y) + P.sky_m[0][2] * fp.z) + P.sky_m[0][3] * 1.0;
     pt.y = ((P.sky_m[1][0] * fp.x + P.sky_m[1][1] * fp.y) + P.sky_m[1][2] * fp.z) + P.sky_m[1][3] * 1.0;
     pt.z = ((P.sky_m[2][0] * fp.x + P.sky_m[2][1] * fp.y) + P.sky_m[2][2] * fp.z) + P.sky_m[2][3] * 1.0;
-    const V3 color = cloud_color_lane(P, S.cloud_z, pt DT_SKY_DBG_ARG(S.stats + ST_DN_OVF));
+    const V3 color = cloud_color_lane(P, S.cloud_z, pt);
     if (valid) {
       store_pixel(P, out, x, y, so, color);
       if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
@@ -3350,7 +3349,7 @@ dt_sky_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   pt.x = ((P.sky_m[0][0] * fp.x + P.sky_m[0][1] * fp.y) + P.sky_m[0][2] * fp.z) + P.sky_m[0][3] * 1.0;
   pt.y = ((P.sky_m[1][0] * fp.x + P.sky_m[1][1] * fp.y) + P.sky_m[1][2] * fp.z) + P.sky_m[1][3] * 1.0;
   pt.z = ((P.sky_m[2][0] * fp.x + P.sky_m[2][1] * fp.y) + P.sky_m[2][2] * fp.z) + P.sky_m[2][3] * 1.0;
-  V3 color = cloud_color_lane(P, zs, pt DT_SKY_DBG_ARG(Lp->S.stats + ST_DN_OVF));
+  V3 color = cloud_color_lane(P, zs, pt);
   store_pixel(P, out, x, y, so, color);
 }
 

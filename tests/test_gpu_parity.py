@@ -147,6 +147,26 @@ def test_final_c5_tunnel_motion_blur(cuda, n):
     assert_parity("final C5 frame %d" % (n * 8), gpu[m], ref[m])
 
 
+@pytest.mark.parametrize("spp,res,build", [(4, (160, 90), "dt_trace_kernel_tunnel"),
+                                           (64, (48, 27), "dt_trace_kernel_w5_tunnel")])
+def test_called_sky_march_tunnel_builds(cuda, spp, res, build):
+    """The tunnel and blur builds march the sky in a called function (dt_kernels.hip DT_SKY_CALL,
+    csrc/Makefile SKYCALL). Under -disable-machine-cse that function returned wrong colours (its
+    1.5 constants encoded as 0): a whole C5 tunnel frame with sky pixels, n = 180
+    (buildFinal(1440), the C5 blur share's frames), on the 4-wave and the 5-wave build, against the
+    oracle."""
+    g = dt.globals_default()
+    g.use_model = 0
+    built = dt.build_scene("final", 1440, g)
+    g.xRes, g.yRes = res
+    g.antialias_samples, g.max_depth = spp, 3
+    assert dt.trace_build(built, g, 1440)[0] == build
+    gpu, st = _render_gpu(built, g, 1440, dt.tiles())
+    ref, rst = oracle.render(built, g, 1440, dt.tiles())
+    assert st.sky_pixels == rst.sky_pixels > 0 and st.rays == rst.rays
+    assert_parity("C5 frame 1440 sky, %s" % build, gpu, ref)
+
+
 @pytest.mark.parametrize("defer", ["1", "0"])
 def test_final_c5_cloud_frame(cuda, monkeypatch, defer):
     """C5 cloud frame buildFinal(2000) (n = 250 >= 244): the builder forces 1 spp and no aperture

@@ -6,6 +6,7 @@ T_1 / (N * max_r T_r) bounds the kernel-side strong-scaling efficiency of bench.
 
     python tools/rank_balance.py [c3|c2|c4] [reps]     (TILE=<side>: the split's tile side, default FrameSplit's for the world size)
 
+WORLDS=8 (or 1,8 ...): only these world sizes (the efficiency then needs world 1 among them).
 INFLIGHT=n (2, 3, ...): each rank's time per frame over 16 frames rendered back to back on n streams with
 one scene object each (bench.py renders two in flight at N > 1), instead of one launch's kernel time.
 """
@@ -48,7 +49,8 @@ def main():
         return best
     from distraytracer_amd.multigpu import tile_side
     t1 = None
-    for world in (1, 2, 4, 8):
+    worlds = [int(v) for v in os.environ.get("WORLDS", "1,2,4,8").split(",")]
+    for world in worlds:
         per, work = [], []
         for rank in (range(world) if not os.environ.get("REVERSE") else reversed(range(world))):
             ts = int(os.environ["TILE"]) if "TILE" in os.environ else tile_side(world)   # as FrameSplit
@@ -69,7 +71,8 @@ def main():
         mx = max(per)
         print(json.dumps({"config": cfg, "world": world, "kernel_ms_per_rank": per, "max_ms": mx,
                           "mean_ms": round(sum(per) / world, 3),
-                          "kernel_efficiency": round(t1 / (world * mx), 4), "rays_shadow_M": work}), flush=True)
+                          "kernel_efficiency": round(t1 / (world * mx), 4) if t1 else None,
+                          "rays_shadow_M": work}), flush=True)
     for sc in scenes:
         sc.close()
 

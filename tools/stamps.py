@@ -49,7 +49,8 @@ def main():
           % (100.0 * arr[32] / max(tot, 1), 100.0 * arr[33] / max(tot, 1)))
     print("shadow grid per item: list tests %.1f, list walks %.2f, cell lookups inside %.2f / outside %.2f, "
           "list too long %.2f" % (arr[34] / items, arr[35] / items, arr[36] / items, arr[38] / items, arr[37] / items))
-    print("scattered shadow waves per item %.2f, union walks %.2f" % (arr[40] / items, arr[41] / items))
+    print("scattered shadow waves per item %.2f, union walks %.2f; with a lane outside the grid %.2f (incl. "
+          "coherent-check outside above)" % (arr[40] / items, arr[41] / items, arr[38] / items))
     print("wave-level shadow prim tests per item by path: cell list %.2f, union %.2f, tree walk %.2f, "
           "block subtree %.2f" % (arr[42] / items, arr[43] / items, arr[44] / items, arr[45] / items))
     print("block-subtree shadow walks per item %.2f (DT_SG_SUBTREE=1)" % (arr[63] / items))
