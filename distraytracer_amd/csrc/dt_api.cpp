@@ -18,6 +18,7 @@ using namespace dth;
 
 extern "C" size_t dt_launch_size(void);
 extern "C" size_t dt_scene_struct_offset(void);
+extern "C" size_t dt_scene_struct_size(void);
 extern "C" size_t dt_params_struct_offset(void);
 extern "C" hipError_t dt_launch_sky(const void* dev_launch, float* out, int64_t n_threads, hipStream_t stream);
 extern "C" hipError_t dt_launch_sky_miss(const void* dev_launch, float* out, int64_t n_px, hipStream_t stream);
@@ -77,6 +78,9 @@ struct HScene {
   unsigned int* again_n;
   const void* sub_nodes;      // shadow-grid block subtrees
   const uint32_t* sub_blocks;
+  unsigned long long* clear0;   // the other parity's counters, zeroed by the launch (dt_kernels.hip)
+  unsigned long long* clear1;
+  int32_t n_clear0, n_clear1;
 };
 
 #define DT_N_STAMPS (64 + 3 * 8 * 256)   // diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters):
@@ -84,6 +88,9 @@ struct HScene {
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
        ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15,
        ST_DONATE = 16, ST_DN_OVF = 17, ST_N = 18 };
+// one parity's counter block: the trace launch's (counters, queue word, stamps slots), the sky-item
+// launch's (counters, queue word, list count)
+constexpr size_t STATS1 = ST_N + 1 + DT_N_STAMPS, STATS2 = ST_N + 2;
 
 int fail(int code, const std::string& msg)
 {
@@ -177,8 +184,15 @@ struct dt_scene {
   void* d_tex = nullptr;
   void* d_zs = nullptr;
   size_t zs_cap = 0;
-  unsigned long long* d_stats = nullptr;   // ST_N counters + queue word
+  // ST_N counters + queue word (+ the stamps builds' slots), twice: launches alternate between the
+  // two (parity), and each zeroes the other for the next one (HScene::clear0)
+  unsigned long long* d_stats = nullptr;
+  int n_launch = 0;     // trace launches enqueued (the parity of the next: n_launch & 1)
+  int last_parity = 0;  // the parity of the last one (dt_collect_stats)
+  // the launch record's device copy, one per parity, uploaded only when its bytes changed (a still
+  // frame rendered again uploads nothing: no copy kernel between its launches)
   void* d_launch = nullptr;
+  std::vector<uint8_t> rec_last[2], rec2_last[2];
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t ev_copy = nullptr;   // staging buffers may be rewritten once this has fired
   uint8_t* h_launch = nullptr;    // pinned staging for the launch record
@@ -202,7 +216,7 @@ struct dt_scene {
   int64_t again_cap = 0;
   void* d_launch2 = nullptr;
   uint8_t* h_launch2 = nullptr;
-  unsigned long long* d_stats2 = nullptr;   // ST_N counters + queue word + list count
+  unsigned long long* d_stats2 = nullptr;   // ST_N counters + queue word + list count, twice (parity)
   bool again_used = false;                  // the last render ran the second launch
   void* d_dn_pool = nullptr;       // dt_trace_kernel_dn: DT_DN_POOL_REC work-sharing records per wave
   int64_t dn_pool_waves = 0;
@@ -403,14 +417,17 @@ static int scene_upload(dt_scene* s)
     release_device(s);
     return rc;
   }
-  if (hipMalloc((void**)&s->d_stats, sizeof(unsigned long long) * (ST_N + 1 + DT_N_STAMPS)) != hipSuccess ||
-      hipMalloc(&s->d_launch, dt_launch_size()) != hipSuccess || hipEventCreate(&s->ev0) != hipSuccess ||
+  if (hipMalloc((void**)&s->d_stats, sizeof(unsigned long long) * 2 * STATS1) != hipSuccess ||
+      hipMemset(s->d_stats, 0, sizeof(unsigned long long) * 2 * STATS1) != hipSuccess ||
+      hipMalloc(&s->d_launch, 2 * dt_launch_size()) != hipSuccess || hipEventCreate(&s->ev0) != hipSuccess ||
       hipEventCreate(&s->ev1) != hipSuccess || hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void**)&s->h_launch, dt_launch_size(), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&s->h_zs, 2048 * sizeof(float), hipHostMallocDefault) != hipSuccess) {
     release_device(s);
     return fail(DT_E_NO_DEVICE, "device allocation failed");
   }
+  s->rec_last[0].clear();
+  s->rec_last[1].clear();
   s->uploaded = true;
   return DT_OK;
 }
@@ -605,6 +622,7 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   P.sgb_by = sc->sg.sub_by;
   P.sgb_nbx = sc->sg.sub_nbx;
   P.sgb_nby = sc->sg.sub_nby;
+  P.sgb_bz = sc->sg.sub_bz > 0 ? sc->sg.sub_bz : 1;
   // DT_SG_SUB_MULTI: a wave whose lanes lie in up to this many blocks walks their subtrees in turn
   // (default 1: only waves within one block); read per render
   const char* smu = getenv("DT_SG_SUB_MULTI");
@@ -820,8 +838,13 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   HScene hs;
   fill_hscene(sc, hs);
   hs.cloud_z = (const float*)sc->d_zs;
-  hs.stats = sc->d_stats;
-  hs.queue = sc->d_stats + ST_N;
+  const int par = sc->n_launch & 1;
+  hs.stats = sc->d_stats + par * STATS1;
+  hs.queue = hs.stats + ST_N;
+  hs.clear0 = sc->d_stats + (1 - par) * STATS1;
+  hs.n_clear0 = (int32_t)STATS1;
+  hs.clear1 = nullptr;
+  hs.n_clear1 = 0;
   const int kernel_choice = sc->kernel;
   Build& kb = choose_build(sc->features, sc->no_cull, kernel_choice, P);
   const bool donate = &kb == &g_dn_build;
@@ -901,8 +924,9 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
       unsigned long long* st2 = nullptr;
       void* dl2 = nullptr;
       uint8_t* hl2 = nullptr;
-      hipError_t e = hipMalloc((void**)&st2, sizeof(unsigned long long) * (ST_N + 2));
-      if (e == hipSuccess) e = hipMalloc(&dl2, dt_launch_size());
+      hipError_t e = hipMalloc((void**)&st2, sizeof(unsigned long long) * 2 * STATS2);
+      if (e == hipSuccess) e = hipMemsetAsync(st2, 0, sizeof(unsigned long long) * 2 * STATS2, st);
+      if (e == hipSuccess) e = hipMalloc(&dl2, 2 * dt_launch_size());
       if (e == hipSuccess) e = hipHostMalloc((void**)&hl2, dt_launch_size(), hipHostMallocDefault);
       if (e != hipSuccess) {
         if (st2) (void)hipFree(st2);
@@ -916,6 +940,8 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
       sc->d_stats2 = st2;
       sc->d_launch2 = dl2;
       sc->h_launch2 = hl2;
+      sc->rec2_last[0].clear();
+      sc->rec2_last[1].clear();
     }
     if (PL.n_items > sc->again_cap) {
       HIPCHK(hipStreamSynchronize(st));
@@ -925,20 +951,35 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
       sc->again_cap = PL.n_items;
     }
     hs.again_list = sc->d_again;
-    hs.again_n = (unsigned int*)(sc->d_stats2 + ST_N + 1);
+    hs.again_n = (unsigned int*)(sc->d_stats2 + par * STATS2 + ST_N + 1);
+  }
+  if (sc->d_stats2) {   // the sky-item counters of the next launch, whether or not it runs one
+    hs.clear1 = sc->d_stats2 + (1 - par) * STATS2;
+    hs.n_clear1 = (int32_t)STATS2;
   }
   PL.donate = donate ? 1 : 0;
   const char* dn_after = getenv("DT_DONATE_AFTER");
   PL.donate_after = dn_after ? atoi(dn_after) : 2;
+  if (sizeof(HScene) != dt_scene_struct_size()) return fail(DT_E_INVALID, "HScene does not match the device DScene");
   memset(sc->h_launch, 0, dt_launch_size());
   memcpy(sc->h_launch + dt_scene_struct_offset(), &hs, sizeof(hs));   // after every hs field is set
   memcpy(sc->h_launch + dt_params_struct_offset(), &PL, sizeof(PL));
   if (nz) HIPCHK(hipMemcpyAsync(sc->d_zs, sc->h_zs, nz * sizeof(float), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(sc->d_launch, sc->h_launch, dt_launch_size(), hipMemcpyHostToDevice, st));
+  const size_t rec_size = dt_launch_size();
+  uint8_t* const d_rec = (uint8_t*)sc->d_launch + par * rec_size;
+  if (sc->rec_last[par].size() != rec_size || memcmp(sc->rec_last[par].data(), sc->h_launch, rec_size) != 0) {
+    HIPCHK(hipMemcpyAsync(d_rec, sc->h_launch, rec_size, hipMemcpyHostToDevice, st));
+    sc->rec_last[par].assign(sc->h_launch, sc->h_launch + rec_size);
+  }
+  uint8_t* const d_rec2 = sc->d_launch2 ? (uint8_t*)sc->d_launch2 + par * rec_size : nullptr;
   if (again) {   // the second launch: the listed items, counters of its own
     HScene hs2 = hs;
-    hs2.stats = sc->d_stats2;
-    hs2.queue = sc->d_stats2 + ST_N;
+    hs2.stats = sc->d_stats2 + par * STATS2;
+    hs2.queue = hs2.stats + ST_N;
+    hs2.clear0 = nullptr;   // the first launch cleared them
+    hs2.n_clear0 = 0;
+    hs2.clear1 = nullptr;
+    hs2.n_clear1 = 0;
     dtd::DParams PL2 = PL;
     PL2.sky_again = 2;
     PL2.item_batch = 1;
@@ -946,24 +987,27 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
     memset(sc->h_launch2, 0, dt_launch_size());
     memcpy(sc->h_launch2 + dt_scene_struct_offset(), &hs2, sizeof(hs2));
     memcpy(sc->h_launch2 + dt_params_struct_offset(), &PL2, sizeof(PL2));
-    HIPCHK(hipMemcpyAsync(sc->d_launch2, sc->h_launch2, dt_launch_size(), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemsetAsync(sc->d_stats2, 0, sizeof(unsigned long long) * (ST_N + 2), st));
+    if (sc->rec2_last[par].size() != rec_size || memcmp(sc->rec2_last[par].data(), sc->h_launch2, rec_size) != 0) {
+      HIPCHK(hipMemcpyAsync(d_rec2, sc->h_launch2, rec_size, hipMemcpyHostToDevice, st));
+      sc->rec2_last[par].assign(sc->h_launch2, sc->h_launch2 + rec_size);
+    }
   }
   HIPCHK(hipEventRecord(sc->ev_copy, st));
   sc->copy_pending = true;
-  HIPCHK(hipMemsetAsync(sc->d_stats, 0, sizeof(unsigned long long) * (ST_N + 1 + DT_N_STAMPS), st));
   HIPCHK(hipEventRecord(sc->ev0, st));
-  HIPCHK(kb.launch(sc->d_launch, out_dev, (int)grid, st));
+  HIPCHK(kb.launch(d_rec, out_dev, (int)grid, st));
+  sc->last_parity = par;
+  sc->n_launch++;
   if (again) {
     if (!kb2.resident) kb2.resident = max_resident_waves(kb2.ptr(), 64);
     // a few listed items in the scenes that use it (room frames: none to a handful): 512 waves
     // start and drain faster than a full persistent grid
     int64_t g2 = grid < kb2.resident ? grid : kb2.resident;
     g2 = g2 < 512 ? g2 : 512;
-    HIPCHK(kb2.launch(sc->d_launch2, out_dev, (int)g2, st));
+    HIPCHK(kb2.launch(d_rec2, out_dev, (int)g2, st));
   }
   sc->again_used = again;
-  if (PL.sky_defer) HIPCHK(dt_launch_sky_miss(sc->d_launch, out_dev, n_px, st));
+  if (PL.sky_defer) HIPCHK(dt_launch_sky_miss(d_rec, out_dev, n_px, st));
   HIPCHK(hipEventRecord(sc->ev1, st));
   sc->timed = true;
   sc->launched = true;
@@ -980,10 +1024,10 @@ int dt_collect_stats(const dt_scene* sc_c, void* stream, dt_stats* stats)
   HIPCHK(hipStreamSynchronize(st));
   if (!stats) return DT_OK;
   unsigned long long h[ST_N];
-  HIPCHK(hipMemcpy(h, sc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(h, sc->d_stats + sc->last_parity * STATS1, sizeof(h), hipMemcpyDeviceToHost));
   if (sc->again_used) {   // the listed items' second launch (dt_kernels.hip DT_SKY_AGAIN)
     unsigned long long h2[ST_N];
-    HIPCHK(hipMemcpy(h2, sc->d_stats2, sizeof(h2), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h2, sc->d_stats2 + sc->last_parity * STATS2, sizeof(h2), hipMemcpyDeviceToHost));
     for (int k = 0; k < ST_N; ++k) h[k] += h2[k];
   }
   memset(stats, 0, sizeof(*stats));
@@ -1319,7 +1363,8 @@ extern "C" int dt_debug_counters(const dt_scene* sc, uint64_t* out, int32_t n)
   if (!sc || !out || n < 0 || n > DT_N_STAMPS) return fail(DT_E_INVALID, "bad arguments");
   if (!sc->uploaded) return fail(DT_E_INVALID, "scene not uploaded (dt_scene_upload)");
   std::vector<unsigned long long> h(ST_N + 1 + DT_N_STAMPS);
-  HIPCHK(hipMemcpy(h.data(), sc->d_stats, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(h.data(), sc->d_stats + sc->last_parity * STATS1, sizeof(unsigned long long) * h.size(),
+                   hipMemcpyDeviceToHost));
   for (int i = 0; i < n; ++i) out[i] = h[ST_N + 1 + i];
   return DT_OK;
 }

@@ -199,6 +199,11 @@ struct DScene {
   unsigned int* again_n;    // ... and their count
   const DNodeDev* sub_nodes;   // shadow-grid block subtrees (host_shadowgrid.cpp; P.sgb_*)
   const uint32_t* sub_blocks;  // (first node, node count) per (light, block); count 0: none
+  // counters of the scene's next launch (the other parity, dt_api.cpp), zeroed by workgroup 0: none of
+  // this launch's waves touches them, so no per-launch memset (a blit kernel) has to run between frames
+  unsigned long long* clear0;
+  unsigned long long* clear1;
+  int32_t n_clear0, n_clear1;
 };
 
 // pow(x, n) for the integer exponents the reference writes as pow(x, 2.0) etc. pow(x, 1) is x
@@ -1338,13 +1343,27 @@ __device__ __forceinline__ bool node_hit(const Walk& w, const DNodeDev& nd, floa
 // their masks straight into SGPRs (llvm.amdgcn.fcmp: ordered <=, >, <=, false for NaN as the C
 // compares), so no per-lane bool is materialised and turned back into a mask. Lanes outside exec
 // get no bit, as with a ballot; the callers run at wave-uniform control flow.
+// The six slab values are compared as the reference's floats, but rounded only after the min/max:
+// f64 -> f32 rounding is monotone, so min/max of the rounded values are the rounded min/max (no NaN
+// on this path). Two conversions instead of six (DT_BOX_F64MINMAX=0: the six-conversion form).
+#ifndef DT_BOX_F64MINMAX
+#define DT_BOX_F64MINMAX 1
+#endif
 __device__ __forceinline__ unsigned long long box_mask_finite(const DNodeDev& b, const RayBox& r, V3 st, float tcull)
 {
+#if DT_BOX_F64MINMAX
+  const double ax = (b.lb[0] - st.x) * r.inv.x, cx = (b.ub[0] - st.x) * r.inv.x;
+  const double ay = (b.lb[1] - st.y) * r.inv.y, cy = (b.ub[1] - st.y) * r.inv.y;
+  const double az = (b.lb[2] - st.z) * r.inv.z, cz = (b.ub[2] - st.z) * r.inv.z;
+  const float tmin = (float)__builtin_fmax(__builtin_fmax(__builtin_fmin(ax, cx), __builtin_fmin(ay, cy)), __builtin_fmin(az, cz));
+  const float tmax = (float)__builtin_fmin(__builtin_fmin(__builtin_fmax(ax, cx), __builtin_fmax(ay, cy)), __builtin_fmax(az, cz));
+#else
   const float ax = (float)((b.lb[0] - st.x) * r.inv.x), cx = (float)((b.ub[0] - st.x) * r.inv.x);
   const float ay = (float)((b.lb[1] - st.y) * r.inv.y), cy = (float)((b.ub[1] - st.y) * r.inv.y);
   const float az = (float)((b.lb[2] - st.z) * r.inv.z), cz = (float)((b.ub[2] - st.z) * r.inv.z);
   const float tmin = fmaxf(fmaxf(fminf(ax, cx), fminf(ay, cy)), fminf(az, cz));
   const float tmax = fminf(fminf(fmaxf(ax, cx), fmaxf(ay, cy)), fmaxf(az, cz));
+#endif
   return __builtin_amdgcn_fcmpf(tmin, tmax, 5 /*OLE*/) & __builtin_amdgcn_fcmpf(tmax, 0.0f, 2 /*OGT*/) &
          __builtin_amdgcn_fcmpf(tmin, tcull, 5 /*OLE*/);
 }
@@ -1942,7 +1961,7 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       if (!w.bump_wave && P.sgb_base[li] >= 0) {
         const bool gin = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.sg_dim[0] &&
                          fy < (float)P.sg_dim[1] && fz < (float)P.sg_dim[2];
-        const int blk = gin ? ((int)fz * P.sgb_nby + (int)fy / P.sgb_by) * P.sgb_nbx + (int)fx / P.sgb_bx : -1;
+        const int blk = gin ? (((int)fz / P.sgb_bz) * P.sgb_nby + (int)fy / P.sgb_by) * P.sgb_nbx + (int)fx / P.sgb_bx : -1;
         const uint2* const recs = (const uint2*)S.sub_blocks + P.sgb_base[li];
         const bool wl = active && !lin;   // lanes in tree-walk cells (or outside the grid: blk < 0)
         unsigned long long rem = __ballot(wl);
@@ -2998,11 +3017,16 @@ extern "C" hipError_t dt_launch_isect(const void* dev_launch, int64_t first, int
 }
 extern "C" const void* dt_isect_kernel_ptr(void) { return (const void*)dt_isect_kernel; }
 #else
+// The launch record: a device copy per counter parity (dt_api.cpp), uploaded only when it changed
 extern "C" __global__ void __launch_bounds__(64, DT_TRACE_MIN_WAVES)
 DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
 {
   const DScene& S = Lp->S;
   const DParams& P = Lp->P;
+  if (blockIdx.x == 0) {
+    for (int i = (int)threadIdx.x; i < S.n_clear0; i += DT_WAVE) S.clear0[i] = 0ull;
+    for (int i = (int)threadIdx.x; i < S.n_clear1; i += DT_WAVE) S.clear1[i] = 0ull;
+  }
   // LDS (one wave per block). nrec holds a lane's shading record across the shadow walks
   // (inside run_pass only); red (per-chunk sample colours) and dens (cloud march chunk) are
   // used after the passes, so they share its space. ocol: the DFS colour accumulator,
@@ -3402,6 +3426,7 @@ extern "C" hipError_t dt_launch_normalize(const double* in, double* out, int64_t
 }
 extern "C" size_t dt_launch_size(void) { return sizeof(DLaunch); }
 extern "C" size_t dt_scene_struct_offset(void) { return offsetof(DLaunch, S); }
+extern "C" size_t dt_scene_struct_size(void) { return sizeof(DScene); }
 extern "C" size_t dt_params_struct_offset(void) { return offsetof(DLaunch, P); }
 
 extern "C" hipError_t dt_launch_sky_miss(const void* dev_launch, float* out, int64_t n_px, hipStream_t stream)

@@ -188,11 +188,12 @@ struct DParams {
   double default_col[3];
   double sun[3];          // sundir.normalized() (cpp:152)
   double sun_outer[3], sun_inner[3], sun_core[3], bluesky[3], redsky[3];
-  // shadow-grid block subtrees (host_internal.h ShadowGrid::sub_*): blocks of sgb_bx x sgb_by x 1
-  // cells, sgb_nbx x sgb_nby per layer; light l's records at sgb_base[l] (-1: none)
+  // shadow-grid block subtrees (host_internal.h ShadowGrid::sub_*): blocks of sgb_bx x sgb_by x sgb_bz
+  // cells, sgb_nbx x sgb_nby per layer of blocks; light l's records at sgb_base[l] (-1: none)
   int32_t sgb_base[DT_MAX_SGRID];
   int32_t sgb_bx, sgb_by, sgb_nbx, sgb_nby;
   int32_t sgb_multi;      // a wave walks the subtrees of up to this many blocks in turn (DT_SG_SUB_MULTI)
+  int32_t sgb_bz;         // the blocks' depth in cells (z; DT_SG_SUB_BLOCK XxYxZ)
 };
 
 #ifndef DT_HD

@@ -48,11 +48,11 @@ struct ShadowGrid {
   std::vector<uint32_t> cells;       // (offset into list | DT_SG_UMBRA, count | DT_SG_WALK) per cell
   std::vector<int32_t> list;         // leaf node indices (reference tree)
   double ypad = 0;                   // lists also hold for blur passes with |shift| <= ypad
-  // Block subtrees (DT_SG_SUBTREE): for each block of sub_bx x sub_by x 1 cells holding a cell that
+  // Block subtrees (DT_SG_SUBTREE): for each block of sub_bx x sub_by x sub_bz cells holding a cell that
   // walks the tree, an SAH tree over the leaves whose box meets the block's swept box to the light
   // (the block's list, uncapped). Pass-0 waves whose lanes all lie in one such block walk it instead
   // of the whole tree (C4's mesh cells).
-  int sub_bx = 0, sub_by = 0, sub_nbx = 0, sub_nby = 0;
+  int sub_bx = 0, sub_by = 0, sub_bz = 1, sub_nbx = 0, sub_nby = 0, sub_nbz = 0;
   int32_t sub_base[DT_MAX_SGRID];        // light l's first block record in sub_blocks (-1: none)
   std::vector<uint32_t> sub_blocks;      // (first node, node count) per block; count 0: none
   std::vector<dtd::DNodeDev> sub_nodes;

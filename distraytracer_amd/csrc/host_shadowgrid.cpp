@@ -787,16 +787,26 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
     const double t_sub = now_ms();
     // DT_SG_SUB_BLOCK: the subtree blocks' size in cells (XxY, default the grid tests' 8x4): smaller
     // blocks hold shorter lists, larger ones serve more scattered waves
-    int SBX = std::max(1, blk_x), SBY = std::max(1, blk_y);
-    if (getenv("DT_SG_SUB_BLOCK") && !sg_parse_block(getenv("DT_SG_SUB_BLOCK"), SBX, SBY))
-      fprintf(stderr, "dt: DT_SG_SUB_BLOCK='%s' not understood (use XxY): 8x4\n", getenv("DT_SG_SUB_BLOCK"));
-    SBX = std::max(1, SBX);
-    SBY = std::max(1, SBY);
+    // (blocks of XxYxZ cells: a scattered wave's lanes on a mesh spread over z as much as over x, y)
+    int SBX = std::max(1, blk_x), SBY = std::max(1, blk_y), SBZ = 1;
+    if (const char* sb = getenv("DT_SG_SUB_BLOCK")) {
+      int x = 0, y = 0, z = 1;
+      const int n = sscanf(sb, "%dx%dx%d", &x, &y, &z);
+      if (n >= 2 && x >= 1 && y >= 1 && z >= 1) {
+        SBX = x;
+        SBY = y;
+        SBZ = n == 3 ? z : 1;
+      } else {
+        fprintf(stderr, "dt: DT_SG_SUB_BLOCK='%s' not understood (use XxY or XxYxZ): %dx%dx1\n", sb, SBX, SBY);
+      }
+    }
     g.sub_bx = SBX;
     g.sub_by = SBY;
+    g.sub_bz = SBZ;
     g.sub_nbx = (g.dim[0] + SBX - 1) / SBX;
     g.sub_nby = (g.dim[1] + SBY - 1) / SBY;
-    const size_t nblk = (size_t)g.sub_nbx * g.sub_nby * g.dim[2];
+    g.sub_nbz = (g.dim[2] + SBZ - 1) / SBZ;
+    const size_t nblk = (size_t)g.sub_nbx * g.sub_nby * g.sub_nbz;
     struct SubItem { int l; size_t blk; };
     std::vector<SubItem> sitems;
     for (size_t l = 0; l < (size_t)DT_MAX_SGRID; ++l) g.sub_base[l] = -1;
@@ -807,7 +817,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       for (int c = 0; c < ncell; ++c)
         if (g.cells[2 * ((size_t)g.base[l] + c) + 1] == DT_SG_WALK) {
           const int x = c % g.dim[0], y = (c / g.dim[0]) % g.dim[1], z = c / (g.dim[0] * g.dim[1]);
-          mark[((size_t)z * g.sub_nby + y / SBY) * g.sub_nbx + x / SBX] = 1;
+          mark[((size_t)(z / SBZ) * g.sub_nby + y / SBY) * g.sub_nbx + x / SBX] = 1;
           any = true;
         }
       if (!any) continue;
@@ -825,10 +835,11 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
         const size_t l = (size_t)sitems[k].l, blk = sitems[k].blk;
         const LightSetup& S = ls[l];
         const dtd::DLight& L = lights[l];
-        const int z = (int)(blk / ((size_t)g.sub_nbx * g.sub_nby));
+        const int bz = (int)(blk / ((size_t)g.sub_nbx * g.sub_nby));
         const int by = (int)((blk / g.sub_nbx) % g.sub_nby), bx = (int)(blk % g.sub_nbx);
-        const int c0[3] = {bx * SBX, by * SBY, z};
-        const int c1[3] = {std::min((bx + 1) * SBX, g.dim[0]) - 1, std::min((by + 1) * SBY, g.dim[1]) - 1, z};
+        const int c0[3] = {bx * SBX, by * SBY, bz * SBZ};
+        const int c1[3] = {std::min((bx + 1) * SBX, g.dim[0]) - 1, std::min((by + 1) * SBY, g.dim[1]) - 1,
+                           std::min((bz + 1) * SBZ, g.dim[2]) - 1};
         double clo[3], chi[3];
         for (int a = 0; a < 3; ++a) {
           clo[a] = lo[a] + c0[a] * hh[a] - m1;

@@ -24,4 +24,15 @@ python tools/overlap.py $O/ovl > $O/overlap.txt 2>&1 || true
 
 DT_SG_SUBTREE=1 DT_LIB=distraytracer_amd/variants/libdt_stamps.so timeout -k 10 300 python tools/stamps.py c4 > $O/stamps_c4_sub.log 2>&1 || echo "stamps c4 failed"
 echo stamps done
+V=distraytracer_amd/variants
+b() {   # name, lib ("" = product), config, steps
+  local lib=""; [ -n "$2" ] && lib="DT_LIB=$V/libdt_$2.so"
+  env $lib timeout -k 10 200 python bench.py --config $3 --steps $4 --warmup 1 --no-cpu-baseline --no-roofline > $O/$1.json 2>/dev/null
+  python -c "import json;d=json.loads(open('$O/$1.json').read().splitlines()[-1]);print('$1',d['value'],d['roofline']['kernel_ms'])" >> $O/ab.txt
+}
+for rep in 1 2; do
+  b c3_bmm0_$rep bmm0 c3 10; b c3_prod_$rep "" c3 10
+  b c2_bmm0_$rep bmm0 c2 10; b c2_prod_$rep "" c2 10
+  b c4_bmm0_$rep bmm0 c4 2; b c4_prod_$rep "" c4 2
+done
 echo all done
