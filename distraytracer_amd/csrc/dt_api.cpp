@@ -83,7 +83,7 @@ struct HScene {
   int32_t n_clear0, n_clear1;
 };
 
-#define DT_N_STAMPS (64 + 3 * 8 * 256)   // diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters):
+#define DT_N_STAMPS (72 + 3 * 8 * 256)   // diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters):
                                          // phases, then (waves, lanes, hits) per (light, shape) shadow test
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
        ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15,
@@ -193,6 +193,7 @@ struct dt_scene {
   // frame rendered again uploads nothing: no copy kernel between its launches)
   void* d_launch = nullptr;
   std::vector<uint8_t> rec_last[2], rec2_last[2];
+  std::vector<float> zs_last;   // the z table in d_zs
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t ev_copy = nullptr;   // staging buffers may be rewritten once this has fired
   uint8_t* h_launch = nullptr;    // pinned staging for the launch record
@@ -428,6 +429,7 @@ static int scene_upload(dt_scene* s)
   }
   s->rec_last[0].clear();
   s->rec_last[1].clear();
+  s->zs_last.clear();
   s->uploaded = true;
   return DT_OK;
 }
@@ -831,6 +833,7 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
     if (sc->d_zs) HIPCHK(hipStreamSynchronize(st));
     if (sc->d_zs) (void)hipFree(sc->d_zs);
     sc->d_zs = nullptr;
+    sc->zs_last.clear();
     sc->zs_cap = 2048;
     HIPCHK(hipMalloc(&sc->d_zs, sc->zs_cap * sizeof(float)));
   }
@@ -964,7 +967,11 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   memset(sc->h_launch, 0, dt_launch_size());
   memcpy(sc->h_launch + dt_scene_struct_offset(), &hs, sizeof(hs));   // after every hs field is set
   memcpy(sc->h_launch + dt_params_struct_offset(), &PL, sizeof(PL));
-  if (nz) HIPCHK(hipMemcpyAsync(sc->d_zs, sc->h_zs, nz * sizeof(float), hipMemcpyHostToDevice, st));
+  // the z table too only when it changed (the same for every frame of a scene's sky)
+  if (nz && (sc->zs_last.size() != nz || memcmp(sc->zs_last.data(), sc->h_zs, nz * sizeof(float)) != 0)) {
+    HIPCHK(hipMemcpyAsync(sc->d_zs, sc->h_zs, nz * sizeof(float), hipMemcpyHostToDevice, st));
+    sc->zs_last.assign(sc->h_zs, sc->h_zs + nz);
+  }
   const size_t rec_size = dt_launch_size();
   uint8_t* const d_rec = (uint8_t*)sc->d_launch + par * rec_size;
   if (sc->rec_last[par].size() != rec_size || memcmp(sc->rec_last[par].data(), sc->h_launch, rec_size) != 0) {

@@ -37,6 +37,7 @@ using namespace dtd;
 #ifdef DT_STAMPS
 #define DT_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define DT_ACC(k, a, b) cnt.ph[k] += (b) - (a)
+#define DT_PH_N 72   // stamp slots (dt_api.cpp DT_N_STAMPS, tools/stamps.py)
 #define DT_CNT(k) cnt.ph[k] += 1   // wave-uniform event count (7 DFS steps, 8 prim tests, 9 lights)
 #else
 #define DT_CNT(k)
@@ -1681,7 +1682,7 @@ __device__ __forceinline__ void shadow_leaf(const DScene& S, const DNodeDev& nd,
     cnt.ph[55 + (type & 7)] += __popcll(om_new);
     {   // per (light, shape): waves, lanes, hits (added by lane 0)
       if ((threadIdx.x & 63) == 0 && sid < 254 && cnt.cur_li < 8) {
-        unsigned long long* h = S.stats + ST_N + 1 + 64 + 3 * (cnt.cur_li * 256 + sid);
+        unsigned long long* h = S.stats + ST_N + 1 + DT_PH_N + 3 * (cnt.cur_li * 256 + sid);
         atomicAdd(h, 1ull);
         atomicAdd(h + 1, (unsigned long long)__popcll(tm));
         atomicAdd(h + 2, (unsigned long long)__popcll(om_new));
@@ -1950,7 +1951,10 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
         return bump_list ? occluded_union<true>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt)
                          : occluded_union<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
       }
-#if DT_HAS(DT_SHAPE_TRIANGLE)
+// (bit 3: DT_SHAPE_TRIANGLE is an enum constant, which #if would read as 0; rounds 4-5 had that, so
+// this block was compiled out of the mesh builds)
+static_assert(DT_SHAPE_TRIANGLE == 3, "DT_HAS(3) below");
+#if DT_HAS(3)
       // Some lanes' cells walk the tree (lists over the cap: C4's mesh cells; with scattered glossy
       // bounces one such lane used to send all 64 down the whole tree). With block subtrees
       // (host_shadowgrid.cpp, DT_SG_SUBTREE; pass-0 waves, every lane inside the grid) the wave is
@@ -1958,7 +1962,9 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
       // tree-walk cells, when they lie in at most P.sgb_multi blocks (DT_SG_SUB_MULTI), walk their
       // blocks' subtrees, one block after another with its own lanes. A block's subtree holds every
       // leaf that can occlude a segment from any of its cells. Otherwise the whole tree as before.
+      DT_CNT(64);   // scattered waves with lanes in tree-walk cells (stamps 64-68: the subtree gates)
       if (!w.bump_wave && P.sgb_base[li] >= 0) {
+        DT_CNT(65);
         const bool gin = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.sg_dim[0] &&
                          fy < (float)P.sg_dim[1] && fz < (float)P.sg_dim[2];
         const int blk = gin ? (((int)fz / P.sgb_bz) * P.sgb_nby + (int)fy / P.sgb_by) * P.sgb_nbx + (int)fx / P.sgb_bx : -1;
@@ -1968,10 +1974,14 @@ __device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool
         int nb = 0;
         while (rem && nb < P.sgb_multi) {
           const int b0 = __builtin_amdgcn_readlane(blk, (int)__builtin_ctzll(rem));
-          if (b0 < 0 || recs[b0].y == 0) break;
+          if (b0 < 0 || recs[b0].y == 0) {
+            DT_CNT(b0 < 0 ? 66 : 67);
+            break;
+          }
           rem &= ~__ballot(wl && blk == b0);
           ++nb;
         }
+        if (rem && nb >= P.sgb_multi) DT_CNT(68);   // lanes in more blocks than sgb_multi
         if (!rem) {
           bool occl = false;
           const bool ll = active && lin;
@@ -2051,7 +2061,7 @@ struct Counters {
   unsigned int* wk;                  // the wave's DT_WK_N event counters (LDS)
 #endif
 #ifdef DT_STAMPS
-  unsigned long long ph[64];   // diagnostic build only: cycles per phase, event counts (wave-uniform)
+  unsigned long long ph[DT_PH_N];   // diagnostic build only: cycles per phase, event counts (wave-uniform)
   int cur_li;                  // light of the current shadow test (per-shape histogram)
   int cur_path;                // shadow path of the current test: 0 cell list, 1 union, 2 tree walk
 #endif
@@ -2780,7 +2790,7 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
         {   // per light: (waves, active lanes, occluded lanes), (cycles)
           const unsigned long long bw = __ballot(walk), bo = __ballot(walk && occl);
           if ((threadIdx.x & 63) == 0 && li < 8) {
-            unsigned long long* h = S.stats + ST_N + 1 + 64 + 3 * (li * 256 + 255);
+            unsigned long long* h = S.stats + ST_N + 1 + DT_PH_N + 3 * (li * 256 + 255);
             atomicAdd(h, 1ull);
             atomicAdd(h + 1, (unsigned long long)__popcll(bw));
             atomicAdd(h + 2, (unsigned long long)__popcll(bo));
@@ -3066,7 +3076,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   cnt.wk = wk_lds;
 #endif
 #ifdef DT_STAMPS
-  for (int k = 0; k < 64; ++k) cnt.ph[k] = 0;
+  for (int k = 0; k < DT_PH_N; ++k) cnt.ph[k] = 0;
   cnt.cur_li = 0;
   cnt.cur_path = 0;
 #endif
@@ -3298,7 +3308,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     if (lane == 0) {
       atomicAdd(S.stats + ST_WNODES, (unsigned long long)cnt.wnodes);
 #ifdef DT_STAMPS
-      for (int k = 0; k < 64; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);
+      for (int k = 0; k < DT_PH_N; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);
 #endif
       if (sky_px) atomicAdd(S.stats + ST_SKY, sky_px);
       atomicAdd(S.stats + ST_RAYS, r);

@@ -26,7 +26,7 @@ def main():
     s = dt.Scene(b, g)
     out = torch.zeros(3 * g.xRes * g.yRes, dtype=torch.float32, device="cuda")
     st = dt.render(s, g, frame, out)
-    NS = 64 + 3 * 8 * 256
+    NS = 72 + 3 * 8 * 256
     arr = (ctypes.c_uint64 * NS)()
     dt.check(dt.lib.dt_debug_counters(s.handle, arr, NS))
     tot = arr[5] + arr[6]
@@ -53,7 +53,10 @@ def main():
           "coherent-check outside above)" % (arr[40] / items, arr[41] / items, arr[38] / items))
     print("wave-level shadow prim tests per item by path: cell list %.2f, union %.2f, tree walk %.2f, "
           "block subtree %.2f" % (arr[42] / items, arr[43] / items, arr[44] / items, arr[45] / items))
-    print("block-subtree shadow walks per item %.2f (DT_SG_SUBTREE=1)" % (arr[63] / items))
+    print("block-subtree shadow walks per item %.2f (DT_SG_SUBTREE=1); gates per item: scattered waves with "
+          "tree-walk lanes %.2f, subtrees built for the light %.2f, a lane outside the grid %.2f, a block without a "
+          "subtree %.2f, more blocks than DT_SG_SUB_MULTI %.2f"
+          % (arr[63] / items, arr[64] / items, arr[65] / items, arr[66] / items, arr[67] / items, arr[68] / items))
     print("shadow walks per item: all occluded %.2f (%.1f visits/walk), none occluded %.2f (%.1f/walk), total %.2f"
           % (arr[29] / items, arr[28] / max(arr[29], 1), arr[31] / items, arr[30] / max(arr[31], 1), arr[9] / items))
     # per (light, shape) shadow tests: wave-level tests per item, lanes per test, lane hit fraction
@@ -61,14 +64,14 @@ def main():
     rows = []
     for li in range(8):
         for sid in range(256):
-            o = 64 + 3 * (li * 256 + sid)
+            o = 72 + 3 * (li * 256 + sid)
             if arr[o]:
                 rows.append((arr[o], li, sid, arr[o + 1], arr[o + 2]))
     rows = [r for r in rows if r[2] < 254]
     rows.sort(reverse=True)
     print("per light: calls/item, active lanes/call, occluded fraction, share of kernel cycles")
     for li in range(8):
-        o = 64 + 3 * (li * 256 + 255)
+        o = 72 + 3 * (li * 256 + 255)
         if arr[o]:
             sw = sum(r[0] for r in rows if r[1] == li)
             sl = sum(r[3] for r in rows if r[1] == li)
