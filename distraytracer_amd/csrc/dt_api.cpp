@@ -195,10 +195,6 @@ struct dt_scene {
   void* d_launch = nullptr;
   std::vector<uint8_t> rec_last[2], rec2_last[2];
   std::vector<float> zs_last;   // the z table in d_zs
-  // DT_TILE_ORDER: the slot order of the rank's share (DParams::slot_order) and what it was built for
-  uint32_t* d_slot_order = nullptr;
-  int64_t slot_order_cap = 0;
-  std::vector<int64_t> slot_order_key;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t ev_copy = nullptr;   // staging buffers may be rewritten once this has fired
   uint8_t* h_launch = nullptr;    // pinned staging for the launch record
@@ -382,7 +378,7 @@ static void release_device(dt_scene* s)
   void** bufs[] = {&s->d_pl_cells, &s->d_pl_list, &s->d_nodes, &s->d_fnodes, &s->d_bnodes, &s->d_bparent,
                    &s->d_sg_cells, &s->d_sg_list, &s->d_sub_nodes, &s->d_sub_blocks, &s->d_leaf, &s->d_hdr, &s->d_geom, &s->d_mat, &s->d_lights,
                    &s->d_tex, &s->d_zs, (void**)&s->d_stats, &s->d_launch, (void**)&s->d_sky_miss, &s->d_dn_pool,
-                   (void**)&s->d_again, &s->d_launch2, (void**)&s->d_stats2, (void**)&s->d_slot_order};
+                   (void**)&s->d_again, &s->d_launch2, (void**)&s->d_stats2};
   for (void** b : bufs) {
     if (*b) (void)hipFree(*b);
     *b = nullptr;
@@ -435,8 +431,6 @@ static int scene_upload(dt_scene* s)
   s->rec_last[0].clear();
   s->rec_last[1].clear();
   s->zs_last.clear();
-  s->slot_order_key.clear();
-  s->slot_order_cap = 0;
   s->uploaded = true;
   return DT_OK;
 }
@@ -914,43 +908,6 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
     }
     PL.sky_defer = 1;
     hs.sky_miss = sc->d_sky_miss;
-  }
-  // DT_TILE_ORDER=morton: the queue hands out the rank's tiles in Morton order of their position
-  // instead of slot order, so the waves in flight work on a compact part of the frame (a 1/8 share's
-  // slots run one tile of every eight along whole tile rows); raster (default): slot order
-  PL.slot_order = nullptr;
-  const char* tord = getenv("DT_TILE_ORDER");
-  if (tord && strcmp(tord, "morton") == 0 && PL.n_owned_tiles > 1) {
-    const std::vector<int64_t> key = {PL.world, PL.rank, PL.tiles_x, PL.n_tiles, PL.n_owned_tiles};
-    if (key != sc->slot_order_key) {
-      std::vector<std::pair<uint64_t, uint32_t>> ord((size_t)PL.n_owned_tiles);
-      for (int64_t k = 0; k < PL.n_owned_tiles; ++k) {
-        const int64_t t = dtd::tile_of(k, PL.rank, PL.world);
-        uint64_t m = ~0ull;   // slots past the last tile go last
-        if (t < PL.n_tiles) {
-          const uint32_t tx = (uint32_t)(t % PL.tiles_x), ty = (uint32_t)(t / PL.tiles_x);
-          m = 0;
-          for (int b = 0; b < 16; ++b) m |= (uint64_t)((tx >> b) & 1u) << (2 * b) | (uint64_t)((ty >> b) & 1u) << (2 * b + 1);
-        }
-        ord[(size_t)k] = {m, (uint32_t)k};
-      }
-      std::stable_sort(ord.begin(), ord.end());
-      std::vector<uint32_t> perm(ord.size());
-      for (size_t k = 0; k < ord.size(); ++k) perm[k] = ord[k].second;
-      if ((int64_t)perm.size() > sc->slot_order_cap) {
-        HIPCHK(hipStreamSynchronize(st));
-        if (sc->d_slot_order) (void)hipFree(sc->d_slot_order);
-        sc->d_slot_order = nullptr;
-        sc->slot_order_cap = 0;
-        HIPCHK(hipMalloc((void**)&sc->d_slot_order, perm.size() * sizeof(uint32_t)));
-        sc->slot_order_cap = (int64_t)perm.size();
-      } else {
-        HIPCHK(hipStreamSynchronize(st));   // an earlier launch may still read the old order
-      }
-      HIPCHK(hipMemcpy(sc->d_slot_order, perm.data(), perm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-      sc->slot_order_key = key;
-    }
-    PL.slot_order = sc->d_slot_order;
   }
   // DT_GENERAL_WALKS=1: every wave takes the exact reference-tree walks that axis-parallel rays
   // take (the tests' check of those rare, out-of-line paths against the product walks)
