@@ -6,7 +6,7 @@ T_1 / (N * max_r T_r) bounds the kernel-side strong-scaling efficiency of bench.
 
     python tools/rank_balance.py [c3|c2|c4] [reps]     (TILE=<side>: the split's tile side, default FrameSplit's for the world size)
 
-WORLDS=8 (or 1,8 ...): only these world sizes (the efficiency then needs world 1 among them).
+RES=3840x2160: the config at another resolution. WORLDS=8 (or 1,8 ...): only these world sizes (the efficiency then needs world 1 among them).
 INFLIGHT=n (2, 3, ...): each rank's time per frame over 16 frames rendered back to back on n streams with
 one scene object each (bench.py renders two in flight at N > 1), instead of one launch's kernel time.
 """
@@ -25,6 +25,8 @@ def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     g, built = bench.build_globals(dt, cfg)
+    if os.environ.get("RES"):   # RES=WxH: the config at another resolution (more items per launch)
+        g.xRes, g.yRes = (int(v) for v in os.environ["RES"].split("x"))
     scene = dt.Scene(built, g)
     inflight = int(os.environ.get("INFLIGHT", "1"))
     scenes = [scene] + [dt.Scene(built, g) for _ in range(max(inflight, 1) - 1)]
