@@ -334,7 +334,12 @@ int64_t dt_slab_floats_max(const dt_globals* g, const dt_tiles* tiles); /* max o
  * Synchronous unless dt_render_async is used. */
 int dt_render(const dt_scene* s, const dt_globals* g, int32_t frame, const dt_tiles* tiles,
               float* out, int32_t out_on_device, void* stream, dt_stats* stats);
-/* enqueue only (device output, no host sync, stats device-side until dt_collect_stats) */
+/* enqueue only (device output, no host sync, stats device-side until dt_collect_stats).
+ * A scene's launches must be ordered: keep one scene object per stream (two frames in flight take
+ * two scene objects, as bench.py does). A scene keeps two launch records and two counter blocks
+ * on the device and alternates between them; each launch clears the other block, and a record is
+ * uploaded only when its bytes change, so repeated renders of a still frame enqueue nothing but
+ * their kernels. dt_collect_stats reports the scene's last launch. */
 int dt_render_async(const dt_scene* s, const dt_globals* g, int32_t frame, const dt_tiles* tiles,
                     float* out_device, void* stream);
 int dt_collect_stats(const dt_scene* s, void* stream, dt_stats* stats);
