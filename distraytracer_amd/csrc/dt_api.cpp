@@ -195,10 +195,6 @@ struct dt_scene {
   void* d_launch = nullptr;
   std::vector<uint8_t> rec_last[2], rec2_last[2];
   std::vector<float> zs_last;   // the z table in d_zs
-  // DT_TILE_ORDER: the slot order of the rank's share (DParams::slot_order) and the file it came from
-  uint32_t* d_slot_order = nullptr;
-  int64_t slot_order_cap = 0;
-  std::string slot_order_src;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t ev_copy = nullptr;   // staging buffers may be rewritten once this has fired
   uint8_t* h_launch = nullptr;    // pinned staging for the launch record
@@ -382,7 +378,7 @@ static void release_device(dt_scene* s)
   void** bufs[] = {&s->d_pl_cells, &s->d_pl_list, &s->d_nodes, &s->d_fnodes, &s->d_bnodes, &s->d_bparent,
                    &s->d_sg_cells, &s->d_sg_list, &s->d_sub_nodes, &s->d_sub_blocks, &s->d_leaf, &s->d_hdr, &s->d_geom, &s->d_mat, &s->d_lights,
                    &s->d_tex, &s->d_zs, (void**)&s->d_stats, &s->d_launch, (void**)&s->d_sky_miss, &s->d_dn_pool,
-                   (void**)&s->d_again, &s->d_launch2, (void**)&s->d_stats2, (void**)&s->d_slot_order};
+                   (void**)&s->d_again, &s->d_launch2, (void**)&s->d_stats2};
   for (void** b : bufs) {
     if (*b) (void)hipFree(*b);
     *b = nullptr;
@@ -435,8 +431,6 @@ static int scene_upload(dt_scene* s)
   s->rec_last[0].clear();
   s->rec_last[1].clear();
   s->zs_last.clear();
-  s->slot_order_src.clear();
-  s->slot_order_cap = 0;
   s->uploaded = true;
   return DT_OK;
 }
@@ -917,44 +911,6 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
     }
     PL.sky_defer = 1;
     hs.sky_miss = sc->d_sky_miss;
-  }
-  // DT_TILE_ORDER=dir:<path> (experiment): the queue hands out the rank's slots in the order of
-  // <path>/order_w<world>_r<rank>_t<tile side>.bin (n_owned_tiles uint32 slot indices, e.g. by
-  // decreasing measured cost, tools/lpt_order.py); without such a file, slot order
-  PL.slot_order = nullptr;
-  const char* tord = getenv("DT_TILE_ORDER");
-  if (tord && strncmp(tord, "dir:", 4) == 0 && PL.n_owned_tiles > 1) {
-    char fn[1024];
-    snprintf(fn, sizeof(fn), "%s/order_w%d_r%d_t%d.bin", tord + 4, PL.world, PL.rank, PL.tw);
-    const std::string src = std::string(fn) + "#" + std::to_string(PL.n_owned_tiles);
-    if (src != sc->slot_order_src) {
-      std::vector<uint32_t> perm((size_t)PL.n_owned_tiles);
-      FILE* fp = fopen(fn, "rb");
-      bool ok = fp && fread(perm.data(), sizeof(uint32_t), perm.size(), fp) == perm.size();
-      if (fp) fclose(fp);
-      std::vector<char> seen(perm.size(), 0);
-      for (size_t k = 0; ok && k < perm.size(); ++k) {
-        ok = perm[k] < perm.size() && !seen[perm[k]];   // a permutation of the slots
-        if (ok) seen[perm[k]] = 1;
-      }
-      if (ok) {
-        if ((int64_t)perm.size() > sc->slot_order_cap) {
-          HIPCHK(hipStreamSynchronize(st));
-          if (sc->d_slot_order) (void)hipFree(sc->d_slot_order);
-          sc->d_slot_order = nullptr;
-          sc->slot_order_cap = 0;
-          HIPCHK(hipMalloc((void**)&sc->d_slot_order, perm.size() * sizeof(uint32_t)));
-          sc->slot_order_cap = (int64_t)perm.size();
-        } else {
-          HIPCHK(hipStreamSynchronize(st));   // an earlier launch may still read the old order
-        }
-        HIPCHK(hipMemcpy(sc->d_slot_order, perm.data(), perm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        sc->slot_order_src = src;
-      } else {
-        sc->slot_order_src.clear();
-      }
-    }
-    if (!sc->slot_order_src.empty()) PL.slot_order = sc->d_slot_order;
   }
   // DT_GENERAL_WALKS=1: every wave takes the exact reference-tree walks that axis-parallel rays
   // take (the tests' check of those rare, out-of-line paths against the product walks)

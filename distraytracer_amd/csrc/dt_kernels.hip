@@ -2858,16 +2858,15 @@ __device__ __forceinline__ void pixel_of(const DParams& P, int64_t q, int& x, in
                                          bool& valid)
 {
   const int64_t tile_px = (int64_t)P.tw * P.th;
-  const int64_t qs = q / tile_px;
-  const int local = (int)(q - qs * tile_px);
-  const int64_t slot = P.slot_order && qs < P.n_owned_tiles ? (int64_t)P.slot_order[qs] : qs;
+  const int64_t slot = q / tile_px;
+  const int local = (int)(q - slot * tile_px);
   int py = local / P.tw, px = local - py * P.tw;
   int64_t t = tile_of(slot, P.rank, P.world);
   int ty = (int)(t / P.tiles_x), tx = (int)(t - (int64_t)ty * P.tiles_x);
   x = P.x0 + tx * P.tw + px;
   y = P.y0 + ty * P.th + py;
   valid = slot < P.n_owned_tiles && t < P.n_tiles && x < P.x1 && y < P.y1;
-  slab_off = (slot * tile_px + local) * 3;
+  slab_off = q * 3;
 }
 
 __device__ __forceinline__ void store_pixel(const DParams& P, float* out, int x, int y, int64_t slab_off, V3 color)

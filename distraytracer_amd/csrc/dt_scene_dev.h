@@ -194,10 +194,6 @@ struct DParams {
   int32_t sgb_bx, sgb_by, sgb_nbx, sgb_nby;
   int32_t sgb_multi;      // a wave walks the subtrees of up to this many blocks in turn (DT_SG_SUB_MULTI)
   int32_t sgb_bz;         // the blocks' depth in cells (z; DT_SG_SUB_BLOCK XxYxZ)
-  // the order in which the queue hands out the rank's slots (device array of n_owned_tiles slot
-  // indices, dt_api.cpp DT_TILE_ORDER), or null: slot order. Only the order changes: every pixel
-  // keeps its slab position, its RNG stream and its colour.
-  const uint32_t* slot_order;
 };
 
 #ifndef DT_HD
