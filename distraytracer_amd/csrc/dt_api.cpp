@@ -859,7 +859,8 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
     return fail(DT_E_INVALID, "no trace-kernel build covers the scene's features");
   if (!kb.resident) kb.resident = max_resident_waves(kb.ptr(), 64);
   const int64_t waves = kb.resident;
-  int64_t grid = P.n_items < waves ? P.n_items : waves;
+  const int64_t n_queue = P.n_items * (P.n_frames > 1 ? P.n_frames : 1);   // dt_render_repeat_async
+  int64_t grid = n_queue < waves ? n_queue : waves;
   if (grid < 1) grid = 1;
   hs.dn_pool = nullptr;
   if (donate) {
@@ -887,8 +888,8 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   // Three per atomic once every wave takes 256 or more (a whole C3 frame: ~405 per wave, +0.6%,
   // profiles/r05q_ab_switches.txt); the 1/8 shares (~50 per wave) keep two, where three cost their
   // bound 2.5% in round 4 (r04zj_ab_batch_policies.log)
-  PL.item_batch = PL.n_items >= batch_from * grid && (PL.chunks == 1 || (bs && atoi(bs) > 0))
-                      ? (bs && atoi(bs) > 0 ? atoi(bs) : (PL.n_items >= 256 * grid ? 3 : 2)) : 1;
+  PL.item_batch = n_queue >= batch_from * grid && (PL.chunks == 1 || (bs && atoi(bs) > 0))
+                      ? (bs && atoi(bs) > 0 ? atoi(bs) : (n_queue >= 256 * grid ? 3 : 2)) : 1;
   // deep-cascade waves raise their priority (dt_kernels.hip, DT_PRIO_STEPS) when the frame is split
   // over ranks, where one such wave bounds a rank's kernel; DT_PRIO_STEPS=<n> overrides (0: off)
   const char* ps = getenv("DT_PRIO_STEPS");
@@ -901,6 +902,7 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   PL.sky_defer = 0;
   hs.sky_miss = nullptr;
   if (defer_on && PL.spp == 1 && PL.perlin_cloud && n_px > 0) {
+    if (PL.n_frames > 1) return fail(DT_E_UNSUPPORTED, "dt_render_repeat_async: 1-spp sky frames (deferred sky)");
     if (n_px > sc->sky_miss_cap) {
       HIPCHK(hipStreamSynchronize(st));
       if (sc->d_sky_miss) (void)hipFree(sc->d_sky_miss);
@@ -950,12 +952,12 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
       sc->rec2_last[0].clear();
       sc->rec2_last[1].clear();
     }
-    if (PL.n_items > sc->again_cap) {
+    if (n_queue > sc->again_cap) {   // (a listed item: copy * n_items + item, dt_kernels.hip)
       HIPCHK(hipStreamSynchronize(st));
       if (sc->d_again) (void)hipFree(sc->d_again);
       sc->d_again = nullptr;
-      HIPCHK(hipMalloc((void**)&sc->d_again, sizeof(uint32_t) * PL.n_items));
-      sc->again_cap = PL.n_items;
+      HIPCHK(hipMalloc((void**)&sc->d_again, sizeof(uint32_t) * n_queue));
+      sc->again_cap = n_queue;
     }
     hs.again_list = sc->d_again;
     hs.again_n = (unsigned int*)(sc->d_stats2 + par * STATS2 + ST_N + 1);
@@ -1096,6 +1098,23 @@ int dt_render_async(const dt_scene* sc_c, const dt_globals* g, int32_t frame, co
   std::vector<float> zs;
   int rc = prepare_render(sc, g, frame, tiles, P, zs);
   if (rc) return rc;
+  return enqueue_render(sc, P, zs, out_device, (hipStream_t)stream);
+}
+
+int dt_render_repeat_async(const dt_scene* sc_c, const dt_globals* g, int32_t frame, const dt_tiles* tiles,
+                           float* out_device, int32_t n_frames, int64_t frame_stride, void* stream)
+{
+  dt_scene* sc = const_cast<dt_scene*>(sc_c);
+  if (!sc || !g || !out_device) return fail(DT_E_INVALID, "null argument");
+  if (n_frames < 1 || (n_frames > 1 && frame_stride < 0)) return fail(DT_E_INVALID, "dt_render_repeat_async: bad n_frames / frame_stride");
+  dtd::DParams P;
+  std::vector<float> zs;
+  int rc = prepare_render(sc, g, frame, tiles, P, zs);
+  if (rc) return rc;
+  if ((double)P.n_items * n_frames >= 4294967296.0)
+    return fail(DT_E_LIMIT, "dt_render_repeat_async: n_frames * items exceeds 2^32");
+  P.n_frames = n_frames;
+  P.frame_stride = frame_stride;
   return enqueue_render(sc, P, zs, out_device, (hipStream_t)stream);
 }
 

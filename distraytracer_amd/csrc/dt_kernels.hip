@@ -3096,8 +3096,11 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   // of every wave is its own by block index: 5120 waves starting at once would otherwise queue
   // behind one another on the one atomic word; the shared counter hands out the items after them.
   const int batch = P.item_batch > 1 ? P.item_batch : 1;
-  // P.sky_again == 2: the queue runs over the items a launch without the sky listed
-  const int64_t n_queue = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)*S.again_n : P.n_items;
+  // P.sky_again == 2: the queue runs over the items a launch without the sky listed. P.n_frames > 1
+  // (dt_render_repeat_async): over that many copies of the frame's items, back to back, so the
+  // copies share one launch and one drain; a listed item carries its copy (copy * n_items + item)
+  const int64_t n_copies = P.n_frames > 1 ? P.n_frames : 1;
+  const int64_t n_queue = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)*S.again_n : P.n_items * n_copies;
   int64_t qpos = (int64_t)blockIdx.x * batch, batch_end = qpos + batch;
   while (true) {
     if (qpos >= batch_end) {
@@ -3108,7 +3111,10 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       __syncthreads();
     }
     if (qpos >= n_queue) break;
-    const int64_t item = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)S.again_list[qpos] : qpos;
+    const int64_t code = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)S.again_list[qpos] : qpos;
+    const int64_t copy = n_copies > 1 ? code / P.n_items : 0;
+    const int64_t item = code - copy * P.n_items;
+    float* const outc = out + copy * P.frame_stride;
     bool sky_again = false;
 #if DT_AGAIN_QUEUE
     // the item's counters are taken back: the launch that listed it counted it already
@@ -3262,16 +3268,16 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
           const int64_t off = P.layout == DT_OUT_SLAB ? qo : 3 * ((int64_t)(P.yRes - 1 - qy) * P.xRes + qx);
 #if DT_ITEM_TIMES == 2   // tools/tail.py: start and end on the 100 MHz clock, 24-bit pieces (exact in f32)
           const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-          out[off] = (float)(uint32_t)(item_t0 & 0xFFFFFF);
-          out[off + 1] = (float)(uint32_t)(t1 & 0xFFFFFF);
-          out[off + 2] = (float)(uint32_t)((t1 >> 24) & 0xFFFFFF);
+          outc[off] = (float)(uint32_t)(item_t0 & 0xFFFFFF);
+          outc[off + 1] = (float)(uint32_t)(t1 & 0xFFFFFF);
+          outc[off + 2] = (float)(uint32_t)((t1 >> 24) & 0xFFFFFF);
 #else
           const float cyc = (float)(__builtin_amdgcn_s_memtime() - item_t0) * 1e-4f;
-          out[off] = cyc; out[off + 1] = cyc; out[off + 2] = cyc;
+          outc[off] = cyc; outc[off + 1] = cyc; outc[off + 2] = cyc;
 #endif
         }
 #else
-        store_pixel(P, out, qx, qy, qo, color);
+        store_pixel(P, outc, qx, qy, qo, color);
 #endif
         if (isnan(color.x) || isnan(color.y) || isnan(color.z)) atomicAdd(S.stats + ST_NAN, 1ull);
       }
@@ -3287,7 +3293,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     }
 #endif
 #if DT_SKY_AGAIN
-    if (item_again && lane == 0) S.again_list[atomicAdd(S.again_n, 1u)] = (uint32_t)item;
+    if (item_again && lane == 0) S.again_list[atomicAdd(S.again_n, 1u)] = (uint32_t)code;
 #endif
     if (P.prio_steps > 0) __builtin_amdgcn_s_setprio(0);
     ++qpos;

@@ -194,6 +194,10 @@ struct DParams {
   int32_t sgb_bx, sgb_by, sgb_nbx, sgb_nby;
   int32_t sgb_multi;      // a wave walks the subtrees of up to this many blocks in turn (DT_SG_SUB_MULTI)
   int32_t sgb_bz;         // the blocks' depth in cells (z; DT_SG_SUB_BLOCK XxYxZ)
+  // dt_render_repeat_async: n_frames copies of the frame's items in one launch, copy f storing into
+  // out + f * frame_stride floats (1: one frame, the default)
+  int32_t n_frames;
+  int64_t frame_stride;
 };
 
 #ifndef DT_HD

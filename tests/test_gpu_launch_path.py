@@ -86,3 +86,25 @@ def test_two_scenes_alternating_streams(cuda):
         st = dt.collect_stats(s)
         assert {k: getattr(st, k) for k in KEYS} == ref_st
         s.close()
+
+
+@pytest.mark.parametrize("built_frame,tiled", [(240, False), (240, True), (1440, False)])
+def test_repeat_launch_copies_equal_single_renders(cuda, built_frame, tiled):
+    """dt_render_repeat_async: n copies of the frame in one launch (one queue over the copies' items,
+    listed sky items carrying their copy) each equal the single render bit for bit; the counters
+    are the copies' sum."""
+    g, b = _globals(built_frame, (160, 96), 4)
+    tile = dt.tiles(tile_w=8, tile_h=8, rank=1, world=4, layout=dt.DT_OUT_SLAB) if tiled else None
+    ref, ref_st = _fresh(b, g, built_frame, tile)
+    n = 3
+    stride = ref.size
+    s = dt.Scene(b, g)
+    big = torch.full((stride * n,), -1.0, dtype=torch.float32, device="cuda")
+    dt.render_repeat_async(s, g, built_frame, big, n, stride, tile)
+    torch.cuda.synchronize()
+    st = dt.collect_stats(s)
+    s.close()
+    got = big.cpu().numpy().reshape(n, stride)
+    for f in range(n):
+        assert np.array_equal(got[f], ref), "copy %d" % f
+    assert st.rays == n * ref_st["rays"] and st.shadow_rays == n * ref_st["shadow_rays"]
