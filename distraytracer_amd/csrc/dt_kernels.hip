@@ -3099,7 +3099,10 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   // P.sky_again == 2: the queue runs over the items a launch without the sky listed. P.n_frames > 1
   // (dt_render_repeat_async): over that many copies of the frame's items, back to back, so the
   // copies share one launch and one drain; a listed item carries its copy (copy * n_items + item)
-  const int64_t n_copies = P.n_frames > 1 ? P.n_frames : 1;
+#ifndef DT_REPEAT   // (A/B switch: 0 compiles the copies out, dt_render_repeat_async then renders one)
+#define DT_REPEAT 1
+#endif
+  const int64_t n_copies = DT_REPEAT && P.n_frames > 1 ? P.n_frames : 1;
   const int64_t n_queue = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)*S.again_n : P.n_items * n_copies;
   int64_t qpos = (int64_t)blockIdx.x * batch, batch_end = qpos + batch;
   while (true) {
@@ -3112,9 +3115,14 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     }
     if (qpos >= n_queue) break;
     const int64_t code = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)S.again_list[qpos] : qpos;
-    const int64_t copy = n_copies > 1 ? code / P.n_items : 0;
-    const int64_t item = code - copy * P.n_items;
-    float* const outc = out + copy * P.frame_stride;
+    int64_t item = code;
+    float* outc = out;
+    if (n_copies > 1) {   // (few copies: subtraction, not a 64-bit division per item)
+      while (item >= P.n_items) {
+        item -= P.n_items;
+        outc += P.frame_stride;
+      }
+    }
     bool sky_again = false;
 #if DT_AGAIN_QUEUE
     // the item's counters are taken back: the launch that listed it counted it already
