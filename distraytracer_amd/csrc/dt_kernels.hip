@@ -470,6 +470,9 @@ __device__ DT_SKY_FN V3 cloud_color_coop(const DParams& P, const float* __restri
   return cloud_finish(P, col);
 }
 
+#ifndef DT_PHILOX_MAD64
+#define DT_PHILOX_MAD64 0
+#endif
 // =====================================================================================
 // counter RNG: Philox4x32-10 (oracle/oracle.c or_philox4x32)
 // =====================================================================================
@@ -478,8 +481,14 @@ __device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, ui
 {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
+#if DT_PHILOX_MAD64   // each product as one 32x32->64 multiply (v_mad_u64_u32) instead of mul_hi + mul_lo
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#else
     uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
     uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+#endif
     uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
