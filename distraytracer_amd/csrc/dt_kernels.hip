@@ -470,8 +470,11 @@ __device__ DT_SKY_FN V3 cloud_color_coop(const DParams& P, const float* __restri
   return cloud_finish(P, col);
 }
 
+// Philox products as one 32x32->64 multiply each (v_mad_u64_u32) instead of mul_hi + mul_lo: C3
+// +0.9%, C2 +0.3%, but C4 -0.6% (the mesh builds keep mul_hi/mul_lo: csrc/Makefile MESH), the same
+// words (profiles/r05y_ab_philox_mad64.txt; round 3, less VALU-bound, measured it neutral)
 #ifndef DT_PHILOX_MAD64
-#define DT_PHILOX_MAD64 0
+#define DT_PHILOX_MAD64 1
 #endif
 // =====================================================================================
 // counter RNG: Philox4x32-10 (oracle/oracle.c or_philox4x32)
@@ -481,7 +484,7 @@ __device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, ui
 {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-#if DT_PHILOX_MAD64   // each product as one 32x32->64 multiply (v_mad_u64_u32) instead of mul_hi + mul_lo
+#if DT_PHILOX_MAD64
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
     uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
