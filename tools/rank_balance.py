@@ -4,7 +4,8 @@ trace-kernel time. With one GPU per rank the frame takes max_r T_r plus the gath
 T_1 / (N * max_r T_r) bounds the kernel-side strong-scaling efficiency of bench.py at N GPUs
 (load balance of the interleaved tiles, the persistent grid's tail on 1/N of the pixels).
 
-    python tools/rank_balance.py [c3|c2|c4] [reps]     (TILE=<side>: the split's tile side, default FrameSplit's for the world size)
+    python tools/rank_balance.py [c3|c2|c4] [reps]     (TILE=<side>: the split's tile side, default FrameSplit's for the world size;
+    TILE_W=<w> TILE_H=<h>: non-square tiles at world > 1)
 
 RES=3840x2160: the config at another resolution. WORLDS=8 (or 1,8 ...): only these world sizes (the efficiency then needs world 1 among them).
 MULTI=n: each rank's time per frame of n copies of the frame in ONE launch (dt_render_repeat_async).
@@ -73,7 +74,10 @@ def main():
         per, work = [], []
         for rank in (range(world) if not os.environ.get("REVERSE") else reversed(range(world))):
             ts = int(os.environ["TILE"]) if "TILE" in os.environ else tile_side(world)   # as FrameSplit
-            tile = dt.tiles(rank=rank, world=world, layout=dt.DT_OUT_SLAB, tile_w=ts, tile_h=ts)
+            tw = th = ts
+            if world > 1 and "TILE_W" in os.environ:   # TILE_W=w TILE_H=h: non-square tiles for world > 1
+                tw, th = int(os.environ["TILE_W"]), int(os.environ["TILE_H"])
+            tile = dt.tiles(rank=rank, world=world, layout=dt.DT_OUT_SLAB, tile_w=tw, tile_h=th)
             out = torch.zeros(max(dt.slab_floats(g, tile), 1), dtype=torch.float32, device="cuda")
             st = dt.render(scene, g, 240, out, tile)   # warm-up
             if multi >= 2:
