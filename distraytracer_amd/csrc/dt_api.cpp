@@ -84,14 +84,14 @@ struct HScene {
   int32_t n_clear0, n_clear1;
 };
 
-#define DT_N_STAMPS (72 + 3 * 8 * 256)   // diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters):
-                                         // phases, then (waves, lanes, hits) per (light, shape) shadow test
+// DT_N_STAMPS (dt_scene_dev.h): diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters):
+// phases, then (waves, lanes, hits) per (light, shape) shadow test
 enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL = 5, ST_PRISM = 6,
        ST_REFL = 7, ST_NAN = 8, ST_PIXELS = 9, ST_SAMPLES = 10, ST_STACK = 11, ST_TEX = 12, ST_BOX = 13, ST_PRIM = 14, ST_WNODES = 15,
        ST_DONATE = 16, ST_DN_OVF = 17, ST_N = 18 };
-// one parity's counter block: the trace launch's (counters, queue word, stamps slots), the sky-item
-// launch's (counters, queue word, list count)
-constexpr size_t STATS1 = ST_N + 1 + DT_N_STAMPS, STATS2 = ST_N + 2;
+// one parity's counter block: the trace launch's (counters, queue word, stamps slots, segment
+// counters), the sky-item launch's (counters, queue word, list count)
+constexpr size_t STATS1 = ST_N + DT_QSEG_OFF + DT_QSEG_MAX * DT_QSEG_STRIDE, STATS2 = ST_N + 2;
 
 int fail(int code, const std::string& msg)
 {
@@ -890,6 +890,13 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   // bound 2.5% in round 4 (r04zj_ab_batch_policies.log)
   PL.item_batch = n_queue >= batch_from * grid && (PL.chunks == 1 || (bs && atoi(bs) > 0))
                       ? (bs && atoi(bs) > 0 ? atoi(bs) : (n_queue >= 256 * grid ? 3 : 2)) : 1;
+  // The queue in 8 contiguous segments, each with its own counter, wave b's home segment b % 8 (the
+  // XCD workgroup b runs on), a drained segment sending its waves on to the next (dt_kernels.hip),
+  // for a rank's share of a split frame: C3's world-8 shares 4.46 against 4.54 ms (bound 0.927
+  // against 0.921, profiles/r05zf_ab_queue_segs.txt). A whole frame keeps one counter: C3 -1.4%,
+  // C4 -3.4%, C2 -0.5% with eight. DT_QUEUE_SEGS=<n> (1..8) overrides.
+  const char* qs = getenv("DT_QUEUE_SEGS");
+  PL.queue_segs = qs ? std::max(1, std::min(atoi(qs), DT_QSEG_MAX)) : (PL.world > 1 ? DT_QSEG_MAX : 1);
   // deep-cascade waves raise their priority (dt_kernels.hip, DT_PRIO_STEPS) when the frame is split
   // over ranks, where one such wave bounds a rank's kernel; DT_PRIO_STEPS=<n> overrides (0: off)
   const char* ps = getenv("DT_PRIO_STEPS");
@@ -996,6 +1003,7 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
     dtd::DParams PL2 = PL;
     PL2.sky_again = 2;
     PL2.item_batch = 1;
+    PL2.queue_segs = 1;
     PL2.prio_steps = 0;
     memset(sc->h_launch2, 0, dt_launch_size());
     memcpy(sc->h_launch2 + dt_scene_struct_offset(), &hs2, sizeof(hs2));

@@ -3116,14 +3116,41 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
 #endif
   const int64_t n_copies = DT_REPEAT && P.n_frames > 1 ? P.n_frames : 1;
   const int64_t n_queue = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)*S.again_n : P.n_items * n_copies;
-  int64_t qpos = (int64_t)blockIdx.x * batch, batch_end = qpos + batch;
+  // P.queue_segs > 1: the queue in that many contiguous segments with a counter each; wave b starts
+  // in segment b % segs (workgroups go round-robin to the XCDs) and takes its first batch there by
+  // block index, then from the segment's counter; a drained segment sends the wave to the next one,
+  // and the wave ends once it has found every segment drained in turn (counters only grow)
+  const int segs = (DT_AGAIN_QUEUE && P.sky_again == 2) || P.queue_segs < 2 ? 1 : P.queue_segs;
+  const int64_t seg_len = (n_queue + segs - 1) / segs;
+  int seg = (int)(blockIdx.x % (unsigned)segs), seg_fails = 0;
+  int64_t seg_lo = seg * seg_len, seg_hi = seg_lo + seg_len < n_queue ? seg_lo + seg_len : n_queue;
+  int64_t qpos = seg_lo + (int64_t)(blockIdx.x / (unsigned)segs) * batch;
+  int64_t batch_end = qpos + batch < seg_hi ? qpos + batch : seg_hi;
   while (true) {
     if (qpos >= batch_end) {
-      if (lane == 0) item_s = atomicAdd(S.queue, (unsigned long long)batch);
-      __syncthreads();
-      qpos = (int64_t)item_s + (int64_t)gridDim.x * batch;
-      batch_end = qpos + batch;
-      __syncthreads();
+      bool drained = false;
+      while (true) {
+        unsigned long long* const ctr = segs == 1 ? S.queue : S.queue + DT_QSEG_OFF + seg * DT_QSEG_STRIDE;
+        if (lane == 0) item_s = atomicAdd(ctr, (unsigned long long)batch);
+        __syncthreads();
+        // the segment's first batches belong to its home waves (blocks seg, seg + segs, ...)
+        const int64_t home = ((int64_t)gridDim.x - seg + segs - 1) / segs;
+        qpos = seg_lo + (int64_t)item_s + home * batch;
+        __syncthreads();
+        if (qpos < seg_hi) {
+          batch_end = qpos + batch < seg_hi ? qpos + batch : seg_hi;
+          seg_fails = 0;
+          break;
+        }
+        if (++seg_fails >= segs) {
+          drained = true;
+          break;
+        }
+        seg = seg + 1 == segs ? 0 : seg + 1;
+        seg_lo = seg * seg_len;
+        seg_hi = seg_lo + seg_len < n_queue ? seg_lo + seg_len : n_queue;
+      }
+      if (drained) break;
     }
     if (qpos >= n_queue) break;
     const int64_t code = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)S.again_list[qpos] : qpos;

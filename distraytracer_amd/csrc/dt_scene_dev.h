@@ -157,6 +157,7 @@ struct DParams {
   int32_t pl_bump;                     // 1: blur-pass lists (bump tree) follow, cells pl_nbx*pl_nby on
   int32_t n_cloud_steps;
   int32_t item_batch;     // wave items per queue atomic (dt_api.cpp: 2 when waves take >= 64 items, else 1)
+  int32_t queue_segs;     // the queue in this many contiguous segments with a counter each (DT_QSEG_*)
   int32_t prio_steps;     // DFS steps after which a wave raises its issue priority (0: never)
   int32_t ls_first;       // first area (rectangle) light: where the light-sample cache starts
   int32_t sky_defer;      // 1 spp: missed pixels are flagged, dt_sky_miss_kernel marches them per lane
@@ -207,6 +208,13 @@ struct DParams {
 #define DT_HD inline
 #endif
 #endif
+
+// The trace launch's counter block (dt_api.cpp STATS1): ST_N counters, the queue word, the stamps
+// builds' slots, then one queue counter per segment, DT_QSEG_STRIDE words apart (own cache lines)
+#define DT_N_STAMPS (72 + 3 * 8 * 256)
+#define DT_QSEG_MAX 8
+#define DT_QSEG_STRIDE 16
+#define DT_QSEG_OFF (1 + DT_N_STAMPS)   // from the queue word
 
 // Tile ownership of the multi-GPU split: the tiles (raster order over the window) fall into groups
 // of `world` consecutive tiles, and slot s of rank r is tile s*world + (r + rot(s)) % world. Every
