@@ -892,11 +892,14 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
                       ? (bs && atoi(bs) > 0 ? atoi(bs) : (n_queue >= 256 * grid ? 3 : 2)) : 1;
   // The queue in 8 contiguous segments, each with its own counter, wave b's home segment b % 8 (the
   // XCD workgroup b runs on), a drained segment sending its waves on to the next (dt_kernels.hip),
-  // for a rank's share of a split frame: C3's world-8 shares 4.46 against 4.54 ms (bound 0.927
-  // against 0.921, profiles/r05zf_ab_queue_segs.txt). A whole frame keeps one counter: C3 -1.4%,
-  // C4 -3.4%, C2 -0.5% with eight. DT_QUEUE_SEGS=<n> (1..8) overrides.
+  // for a rank's share of a split frame of one-chunk items: C3's world-8 shares 4.46 against 4.54 ms
+  // (bound 0.933 against 0.921, profiles/r05zg_rank_balance_segs_default.log), C2's 0.569 against
+  // 0.591. A whole frame keeps one counter (C3 -1.4%, C4 -3.4%, C2 -0.5% with eight), and so do
+  // multi-chunk items (C4's world-8 shares 49.4 against 47.1 ms with eight, profiles/r05zi_*).
+  // DT_QUEUE_SEGS=<n> (1..8) overrides.
   const char* qs = getenv("DT_QUEUE_SEGS");
-  PL.queue_segs = qs ? std::max(1, std::min(atoi(qs), DT_QSEG_MAX)) : (PL.world > 1 ? DT_QSEG_MAX : 1);
+  PL.queue_segs = qs ? std::max(1, std::min(atoi(qs), DT_QSEG_MAX))
+                     : (PL.world > 1 && PL.chunks == 1 ? DT_QSEG_MAX : 1);
   // deep-cascade waves raise their priority (dt_kernels.hip, DT_PRIO_STEPS) when the frame is split
   // over ranks, where one such wave bounds a rank's kernel; DT_PRIO_STEPS=<n> overrides (0: off)
   const char* ps = getenv("DT_PRIO_STEPS");
