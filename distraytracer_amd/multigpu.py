@@ -5,7 +5,7 @@ consecutive tiles (raster order), the ranks rotated by a hash of the group (dt_s
 tile_of), into a packed slab: the expensive sky/glossy regions spread over all GPUs, and unlike a
 plain t % world interleave no rank is tied to a fixed set of tile columns. The tile side follows
 the world size (tile_side): 8x8 (the primary lists' block) at every N > 1, where many tiles per
-rank even out the ranks' work. Rank-balance kernel times of C3 (profiles/r04zs_rank_balance_tiles.log,
+rank even out the ranks' work, and 16x16 for pixels of several 64-sample chunks (spp > 64, C4). Rank-balance kernel times of C3 (profiles/r04zs_rank_balance_tiles.log,
 slowest share 8x8 against 16x16): N=2 17.60 against 17.75 ms, N=4 9.09 against 9.12, N=8 4.73
 against 4.87 (round 3: slowest rank 6.29 -> 5.96 ms from 32x32, profiles/r03z_rank_balance_tiles.log).
 32x32 at N = 1, where the waves that run at once cover a compact part of the image: at world 1 the
@@ -19,15 +19,21 @@ image is bit-identical for any world size.
 from . import DT_OUT_SLAB, slab_floats_max, tiles, unpack_slabs
 
 
-def tile_side(world):
-    """the split's tile side for a world size (module docstring)"""
-    return 32 if world <= 1 else 8
+def tile_side(world, spp=64):
+    """the split's tile side for a world size and samples per pixel (module docstring). Pixels of
+    several 64-sample chunks (spp > 64) take 16x16 at N > 1: C4's bound 0.980 / 0.944 / 0.790 at
+    N = 2 / 4 / 8 against 0.970 / 0.939 / 0.764 with 8x8, twice each
+    (profiles/r05zl_rank_balance_c4_tiles.log)."""
+    if world <= 1:
+        return 32
+    return 16 if spp > 64 else 8
 
 
 class FrameSplit:
     def __init__(self, g, world, rank, tile_w=None, tile_h=None):
-        tile_w = tile_w or tile_side(world)
-        tile_h = tile_h or tile_side(world)
+        spp = getattr(g, "antialias_samples", 64)
+        tile_w = tile_w or tile_side(world, spp)
+        tile_h = tile_h or tile_side(world, spp)
         self.g = g
         self.world = world
         self.rank = rank

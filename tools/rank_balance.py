@@ -73,7 +73,7 @@ def main():
     for world in worlds:
         per, work = [], []
         for rank in (range(world) if not os.environ.get("REVERSE") else reversed(range(world))):
-            ts = int(os.environ["TILE"]) if "TILE" in os.environ else tile_side(world)   # as FrameSplit
+            ts = int(os.environ["TILE"]) if "TILE" in os.environ else tile_side(world, g.antialias_samples)   # as FrameSplit
             tw = th = ts
             if world > 1 and "TILE_W" in os.environ:   # TILE_W=w TILE_H=h: non-square tiles for world > 1
                 tw, th = int(os.environ["TILE_W"]), int(os.environ["TILE_H"])
