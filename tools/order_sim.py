@@ -39,7 +39,7 @@ def main():
     g, built = bench.build_globals(dt, cfg)
     s = dt.Scene(built, g)
     for world in worlds:
-        ts = tile_side(world)
+        ts = tile_side(world, g.antialias_samples)   # as FrameSplit
         tile = dt.tiles(rank=0, world=world, layout=dt.DT_OUT_SLAB, tile_w=ts, tile_h=ts)
         nf = max(dt.slab_floats(g, tile), 1)
         out = torch.zeros(nf, dtype=torch.float32, device="cuda")
