@@ -155,17 +155,6 @@ def render_async(scene, g, frame, out_device, tile=None, stream=None):
                               ctypes.c_void_p(stream) if stream else None), "dt_render_async")
 
 
-def render_repeat_async(scene, g, frame, out_device, n_frames, frame_stride, tile=None, stream=None):
-    """The same frame n_frames times in one launch (dt_render_repeat_async): copy f into
-    out_device[f * frame_stride:]."""
-    p, dev = _ptr(out_device)
-    if not dev:
-        raise DTError("render_repeat_async needs a device output")
-    check(lib.dt_render_repeat_async(scene.handle, ctypes.byref(g), int(frame), ctypes.byref(tile) if tile else None, p,
-                                     int(n_frames), int(frame_stride), ctypes.c_void_p(stream) if stream else None),
-          "dt_render_repeat_async")
-
-
 def collect_stats(scene, stream=None):
     st = Stats()
     check(lib.dt_collect_stats(scene.handle, ctypes.c_void_p(stream) if stream else None, ctypes.byref(st)),

@@ -23,7 +23,7 @@ DT_KERNEL_AUTO, DT_KERNEL_PRODUCT, DT_KERNEL_DONATE = 0, 1, 2   # dt_scene_set_k
 
 SHAPE_TYPES = {1: "sphere", 2: "cylinder", 3: "triangle", 4: "rectangle", 5: "rectprism_v2",
                6: "checkerboard", 7: "checkerboard_hole", 8: "checker_cylinder", 9: "rectprism_cyl"}
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class ShapeDesc(ctypes.Structure):
@@ -117,7 +117,7 @@ class AccelInfo(ctypes.Structure):
 EXPORTS = ["dt_abi_version", "dt_last_error", "dt_globals_default", "dt_scene_create", "dt_scene_destroy",
            "dt_scene_prepare", "dt_scene_upload", "dt_scene_set_kernel",
            "dt_scene_bvh", "dt_bvh_build", "dt_accel_info_build", "dt_trace_build", "dt_slab_floats", "dt_slab_floats_max",
-           "dt_render", "dt_render_async", "dt_render_repeat_async", "dt_collect_stats", "dt_debug_counters", "dt_render_sky",
+           "dt_render", "dt_render_async", "dt_collect_stats", "dt_debug_counters", "dt_render_sky",
            "dt_unpack_slabs", "dt_build_scene", "dt_scene_desc_free", "dt_write_ppm", "dt_write_png",
            "dt_mocap_bone_table", "dt_debug_normalize", "dt_intersect_primary",
            "dt_debug_load_obj"]
@@ -172,8 +172,6 @@ def _load():
                                 ctypes.c_void_p, P(Stats)]),
         "dt_render_async": (c_int32, [ctypes.c_void_p, P(Globals), c_int32, P(Tiles), ctypes.c_void_p,
                                       ctypes.c_void_p]),
-        "dt_render_repeat_async": (c_int32, [ctypes.c_void_p, P(Globals), c_int32, P(Tiles), ctypes.c_void_p,
-                                             c_int32, c_int64, ctypes.c_void_p]),
         "dt_collect_stats": (c_int32, [ctypes.c_void_p, ctypes.c_void_p, P(Stats)]),
         "dt_debug_counters": (c_int32, [ctypes.c_void_p, P(c_uint64), c_int32]),
         "dt_debug_normalize": (c_int32, [P(c_double), P(c_double), c_int64]),

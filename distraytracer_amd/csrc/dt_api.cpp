@@ -82,6 +82,8 @@ struct HScene {
   unsigned long long* clear0;   // the other parity's counters, zeroed by the launch (dt_kernels.hip)
   unsigned long long* clear1;
   int32_t n_clear0, n_clear1;
+  double* chunk_cols;           // chunk items: per-pixel sample colours and arrival words (dt_kernels.hip)
+  unsigned int* chunk_arrive;
 };
 
 // DT_N_STAMPS (dt_scene_dev.h): diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters):
@@ -222,6 +224,9 @@ struct dt_scene {
   bool again_used = false;                  // the last render ran the second launch
   void* d_dn_pool = nullptr;       // dt_trace_kernel_dn: DT_DN_POOL_REC work-sharing records per wave
   int64_t dn_pool_waves = 0;
+  double* d_chunk_cols = nullptr;          // chunk items: spp sample colours per pixel item
+  unsigned int* d_chunk_arrive = nullptr;  // ... and one arrival word per pixel item (kept zero between launches)
+  int64_t chunk_cols_cap = 0, chunk_arrive_cap = 0;
   PrimLists pl;
   bool pl_ok = false;
   void* d_pl_cells = nullptr;
@@ -378,7 +383,8 @@ static void release_device(dt_scene* s)
   void** bufs[] = {&s->d_pl_cells, &s->d_pl_list, &s->d_nodes, &s->d_fnodes, &s->d_bnodes, &s->d_bparent,
                    &s->d_sg_cells, &s->d_sg_list, &s->d_sub_nodes, &s->d_sub_blocks, &s->d_leaf, &s->d_hdr, &s->d_geom, &s->d_mat, &s->d_lights,
                    &s->d_tex, &s->d_zs, (void**)&s->d_stats, &s->d_launch, (void**)&s->d_sky_miss, &s->d_dn_pool,
-                   (void**)&s->d_again, &s->d_launch2, (void**)&s->d_stats2};
+                   (void**)&s->d_again, &s->d_launch2, (void**)&s->d_stats2, (void**)&s->d_chunk_cols,
+                   (void**)&s->d_chunk_arrive};
   for (void** b : bufs) {
     if (*b) (void)hipFree(*b);
     *b = nullptr;
@@ -398,6 +404,7 @@ static void release_device(dt_scene* s)
   s->zs_cap = 0;
   s->sky_miss_cap = 0;
   s->dn_pool_waves = 0;
+  s->chunk_cols_cap = s->chunk_arrive_cap = 0;
   s->copy_pending = s->timed = s->launched = false;
   s->pl_dirty = true;   // the primary lists go up again with the next upload
 }
@@ -859,7 +866,38 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
     return fail(DT_E_INVALID, "no trace-kernel build covers the scene's features");
   if (!kb.resident) kb.resident = max_resident_waves(kb.ptr(), 64);
   const int64_t waves = kb.resident;
-  const int64_t n_queue = P.n_items * (P.n_frames > 1 ? P.n_frames : 1);   // dt_render_repeat_async
+  // Chunk items (spp > 64: C4's 256): every 64-sample chunk of a pixel is a queue item of its own, so
+  // a pixel's chunks run on different waves and a long pixel no longer holds one wave for four
+  // chunks in turn; the chunk that completes a pixel adds its spp sample colours in sample order
+  // (dt_kernels.hip). DT_CHUNK_ITEMS=0 / 1 / 2 (2: the queue chunk-major) overrides the default.
+  const char* ci_env = getenv("DT_CHUNK_ITEMS");
+  int chunk_items = ci_env ? atoi(ci_env) : 1;
+  // (the build and, for a sky-item launch, its *_sky build must carry the code: trait bit 1)
+  if (!(kb.traits() & 2) || !(kb2.traits() & 2) || P.chunks < 2 || P.chunks > 255 ||
+      chunk_items < 0 || chunk_items > 2 ||
+      (double)P.n_items * P.chunks >= 4294967296.0)
+    chunk_items = 0;
+  P.chunk_items = chunk_items;
+  if (chunk_items) {
+    const int64_t n_cols = P.n_items * (int64_t)P.spp * 3;
+    if (n_cols > sc->chunk_cols_cap || P.n_items > sc->chunk_arrive_cap) {
+      HIPCHK(hipStreamSynchronize(st));
+      if (sc->d_chunk_cols) (void)hipFree(sc->d_chunk_cols);
+      if (sc->d_chunk_arrive) (void)hipFree(sc->d_chunk_arrive);
+      sc->d_chunk_cols = nullptr;
+      sc->d_chunk_arrive = nullptr;
+      sc->chunk_cols_cap = sc->chunk_arrive_cap = 0;
+      HIPCHK(hipMalloc((void**)&sc->d_chunk_cols, sizeof(double) * (size_t)n_cols));
+      HIPCHK(hipMalloc((void**)&sc->d_chunk_arrive, sizeof(unsigned int) * (size_t)P.n_items));
+      // zero once: the wave that completes a pixel zeroes its word again
+      HIPCHK(hipMemsetAsync(sc->d_chunk_arrive, 0, sizeof(unsigned int) * (size_t)P.n_items, st));
+      sc->chunk_cols_cap = n_cols;
+      sc->chunk_arrive_cap = P.n_items;
+    }
+  }
+  hs.chunk_cols = chunk_items ? sc->d_chunk_cols : nullptr;
+  hs.chunk_arrive = chunk_items ? sc->d_chunk_arrive : nullptr;
+  const int64_t n_queue = P.n_items * (chunk_items ? P.chunks : 1);
   int64_t grid = n_queue < waves ? n_queue : waves;
   if (grid < 1) grid = 1;
   hs.dn_pool = nullptr;
@@ -912,7 +950,6 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   PL.sky_defer = 0;
   hs.sky_miss = nullptr;
   if (defer_on && PL.spp == 1 && PL.perlin_cloud && n_px > 0) {
-    if (PL.n_frames > 1) return fail(DT_E_UNSUPPORTED, "dt_render_repeat_async: 1-spp sky frames (deferred sky)");
     if (n_px > sc->sky_miss_cap) {
       HIPCHK(hipStreamSynchronize(st));
       if (sc->d_sky_miss) (void)hipFree(sc->d_sky_miss);
@@ -962,7 +999,7 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
       sc->rec2_last[0].clear();
       sc->rec2_last[1].clear();
     }
-    if (n_queue > sc->again_cap) {   // (a listed item: copy * n_items + item, dt_kernels.hip)
+    if (n_queue > sc->again_cap) {   // (a listed item: its queue code, dt_kernels.hip)
       HIPCHK(hipStreamSynchronize(st));
       if (sc->d_again) (void)hipFree(sc->d_again);
       sc->d_again = nullptr;
@@ -1109,23 +1146,6 @@ int dt_render_async(const dt_scene* sc_c, const dt_globals* g, int32_t frame, co
   std::vector<float> zs;
   int rc = prepare_render(sc, g, frame, tiles, P, zs);
   if (rc) return rc;
-  return enqueue_render(sc, P, zs, out_device, (hipStream_t)stream);
-}
-
-int dt_render_repeat_async(const dt_scene* sc_c, const dt_globals* g, int32_t frame, const dt_tiles* tiles,
-                           float* out_device, int32_t n_frames, int64_t frame_stride, void* stream)
-{
-  dt_scene* sc = const_cast<dt_scene*>(sc_c);
-  if (!sc || !g || !out_device) return fail(DT_E_INVALID, "null argument");
-  if (n_frames < 1 || (n_frames > 1 && frame_stride < 0)) return fail(DT_E_INVALID, "dt_render_repeat_async: bad n_frames / frame_stride");
-  dtd::DParams P;
-  std::vector<float> zs;
-  int rc = prepare_render(sc, g, frame, tiles, P, zs);
-  if (rc) return rc;
-  if ((double)P.n_items * n_frames >= 4294967296.0)
-    return fail(DT_E_LIMIT, "dt_render_repeat_async: n_frames * items exceeds 2^32");
-  P.n_frames = n_frames;
-  P.frame_stride = frame_stride;
   return enqueue_render(sc, P, zs, out_device, (hipStream_t)stream);
 }
 

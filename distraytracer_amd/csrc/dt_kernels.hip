@@ -109,6 +109,12 @@ using namespace dtd;
 #define DT_SKY_AGAIN 0
 #endif
 #define DT_AGAIN_QUEUE DT_SKY_BUILD
+// DT_CHUNK_ITEMS=1: the build can run chunk items (P.chunk_items, spp > 64: a pixel's 64-sample chunks
+// on different waves). The room builds (C2, C3, C5's room frames: never more than 64 spp) leave the
+// code out (5-wave room build: +3 VGPR, +24 SGPR spills with it); dt_api.cpp reads the trait bit.
+#ifndef DT_CHUNK_ITEMS
+#define DT_CHUNK_ITEMS 1
+#endif
 // DT_FEATURES: the scene features a build handles (dt_scene_dev.h: bit t for shape type t,
 // DT_FEAT_SPHL sphere lights and emitters, DT_FEAT_RECTL rectangle lights and emitters, DT_FEAT_ON
 // Oren-Nayar, DT_FEAT_GLASS refraction). A build without some of them has those cases compiled out;
@@ -205,6 +211,10 @@ struct DScene {
   unsigned long long* clear0;
   unsigned long long* clear1;
   int32_t n_clear0, n_clear1;
+  // P.chunk_items (spp > 64): per pixel item, its spp sample colours (3 doubles each, sample order),
+  // published by the chunk items that traced them, and its arrival word (dt_trace kernel item loop)
+  double* chunk_cols;
+  unsigned int* chunk_arrive;
 };
 
 // pow(x, n) for the integer exponents the reference writes as pow(x, 2.0) etc. pow(x, 1) is x
@@ -3108,14 +3118,9 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   // of every wave is its own by block index: 5120 waves starting at once would otherwise queue
   // behind one another on the one atomic word; the shared counter hands out the items after them.
   const int batch = P.item_batch > 1 ? P.item_batch : 1;
-  // P.sky_again == 2: the queue runs over the items a launch without the sky listed. P.n_frames > 1
-  // (dt_render_repeat_async): over that many copies of the frame's items, back to back, so the
-  // copies share one launch and one drain; a listed item carries its copy (copy * n_items + item)
-#ifndef DT_REPEAT   // (A/B switch: 0 compiles the copies out, dt_render_repeat_async then renders one)
-#define DT_REPEAT 1
-#endif
-  const int64_t n_copies = DT_REPEAT && P.n_frames > 1 ? P.n_frames : 1;
-  const int64_t n_queue = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)*S.again_n : P.n_items * n_copies;
+  // P.sky_again == 2: the queue runs over the items a launch without the sky listed
+  const int64_t n_queue = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)*S.again_n
+                                                             : P.n_items * (P.chunk_items ? P.chunks : 1);
   // P.queue_segs > 1: the queue in that many contiguous segments with a counter each; wave b starts
   // in segment b % segs (workgroups go round-robin to the XCDs) and takes its first batch there by
   // block index, then from the segment's counter; a drained segment sends the wave to the next one,
@@ -3155,13 +3160,24 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     if (qpos >= n_queue) break;
     const int64_t code = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)S.again_list[qpos] : qpos;
     int64_t item = code;
-    float* outc = out;
-    if (n_copies > 1) {   // (few copies: subtraction, not a 64-bit division per item)
-      while (item >= P.n_items) {
-        item -= P.n_items;
-        outc += P.frame_stride;
+    float* const outc = out;
+    // P.chunk_items: the item is one 64-sample chunk of a pixel item (a listed sky item likewise)
+    int chunk_lo = 0, chunk_hi = P.chunks;
+    if (DT_CHUNK_ITEMS && P.chunk_items) {
+      const uint32_t nck = (uint32_t)P.chunks, ci = (uint32_t)item;
+      uint32_t pi, ck;
+      if (P.chunk_items == 2) {   // chunk-major (host: n_items * chunks < 2^32)
+        ck = ci / (uint32_t)P.n_items;
+        pi = ci - ck * (uint32_t)P.n_items;
+      } else {
+        pi = ci / nck;
+        ck = ci - pi * nck;
       }
+      item = pi;
+      chunk_lo = (int)ck;
+      chunk_hi = chunk_lo + 1;
     }
+    bool px_done = true;   // chunk items: this chunk completed its pixel (it stores it)
     bool sky_again = false;
 #if DT_AGAIN_QUEUE
     // the item's counters are taken back: the launch that listed it counted it already
@@ -3185,7 +3201,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     const unsigned long long item_t0 = DT_ITEM_TIMES == 2 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
 #endif
 
-    for (int chunk = 0; chunk < P.chunks; ++chunk) {
+    for (int chunk = chunk_lo; chunk < chunk_hi; ++chunk) {
       const int sample = chunk * DT_WAVE + (lane - j * per);
       const bool valid = j < group && px_valid && sample < spp && (lane - j * per) < per;
       c.rng.pixel = (uint32_t)(px_y * P.xRes + px_x);
@@ -3275,13 +3291,65 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       }
       DT_T(k2);
       DT_ACC(6, k1, k2);
-      // ordered per-pixel sum (cpp:1212: color += tmp_color in sample order)
-      red[lane * 3 + 0] = tmp_color.x;
-      red[lane * 3 + 1] = tmp_color.y;
-      red[lane * 3 + 2] = tmp_color.z;
-      __syncthreads();
-      {
-        int ns = spp - chunk * DT_WAVE;
+      // ordered per-pixel sum (cpp:1212: color += tmp_color in sample order). red takes this chunk's
+      // sample colours; for chunk items, once this chunk completed its pixel, the pixel's chunks in turn
+      int ck_lo = chunk, ck_hi = chunk + 1;
+      typedef __attribute__((address_space(1))) unsigned long long gu64;
+      typedef __attribute__((address_space(1))) unsigned int gu32;
+      if (DT_CHUNK_ITEMS && P.chunk_items) {
+        // The chunk publishes its 64 sample colours in the pixel's slot and arrives on the pixel's
+        // word; the chunk that completes the pixel adds all spp colours in sample order, the same
+        // additions in the same order as one wave running the chunks in turn. Hand-off across
+        // workgroups and XCDs: write-through (sc1) stores, every lane's stores drained before the
+        // agent-scope arrival; the completing wave acquires at agent scope before its plain loads.
+        // Arrival word: bits 0-15 chunks arrived, 16-23 chunks listed for the sky launch
+        // (P.sky_again 1), 24-31 listed chunks arrived in that launch (P.sky_again 2). The wave
+        // that completes the pixel zeroes the word for the next launch.
+        gu64* const slot = (gu64*)(S.chunk_cols + ((int64_t)item * spp + chunk * DT_WAVE + lane) * 3);
+        if (valid) {
+          __hip_atomic_store(slot, (unsigned long long)__double_as_longlong(tmp_color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(slot + 1, (unsigned long long)__double_as_longlong(tmp_color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(slot + 2, (unsigned long long)__double_as_longlong(tmp_color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const uint32_t add1 = P.sky_again == 2 ? (1u << 24) : 1u + (sky_again ? (1u << 16) : 0u);
+        if (lane == 0)
+          item_s = __hip_atomic_fetch_add((gu32*)(S.chunk_arrive + item), add1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t w = (uint32_t)item_s + add1;
+        px_done = P.sky_again == 2 ? (w >> 24) == ((w >> 16) & 0xFFu)
+                                   : (w & 0xFFFFu) == (uint32_t)P.chunks && (w >> 16) == 0;
+        __syncthreads();
+        ck_lo = 0;
+        ck_hi = px_done ? P.chunks : 0;
+        if (px_done) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+        }
+      }
+#if DT_CHUNK_ITEMS
+      for (int ck = ck_lo; ck < ck_hi; ++ck) {
+#else
+      {   // (a loop of one trip would stay a loop: -fno-unroll-loops)
+        const int ck = chunk;
+        (void)ck_lo; (void)ck_hi;
+#endif
+        if (DT_CHUNK_ITEMS && P.chunk_items) {
+          const double* const src = S.chunk_cols + ((int64_t)item * spp + ck * DT_WAVE + lane) * 3;
+          if (ck * DT_WAVE + lane < spp) {
+            red[lane * 3 + 0] = src[0];
+            red[lane * 3 + 1] = src[1];
+            red[lane * 3 + 2] = src[2];
+          }
+        } else {
+          red[lane * 3 + 0] = tmp_color.x;
+          red[lane * 3 + 1] = tmp_color.y;
+          red[lane * 3 + 2] = tmp_color.z;
+        }
+        __syncthreads();
+        int ns = spp - ck * DT_WAVE;
         if (ns > per) ns = per;
         if (group * 3 <= DT_WAVE) {
           // lane 3 jj + ch sums channel ch of pixel jj: the three channels' chains run side by side
@@ -3298,12 +3366,14 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
           for (int s = 0; s < ns; ++s) ps = add(ps, v3(red[(base + s) * 3], red[(base + s) * 3 + 1], red[(base + s) * 3 + 2]));
           psum[0][lane] = ps.x; psum[1][lane] = ps.y; psum[2][lane] = ps.z;
         }
+        __syncthreads();
       }
-      __syncthreads();
+      if (DT_CHUNK_ITEMS && P.chunk_items && px_done && lane == 0)
+        __hip_atomic_store((gu32*)(S.chunk_arrive + item), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     DT_T(k3);
     const bool item_again = sky_again;
-    if (lane < group) {
+    if (lane < group && px_done) {
       int qx, qy;
       int64_t qo;
       bool qv;
@@ -3528,11 +3598,12 @@ extern "C" hipError_t DT_CAT(DT_TRACE_KERNEL, _launch)(const void* dev_launch, f
   return hipGetLastError();
 }
 extern "C" const void* DT_CAT(DT_TRACE_KERNEL, _ptr)(void) { return (const void*)DT_TRACE_KERNEL; }
-// bit 0: the build lists sky items for another launch (DT_SKY_AGAIN); bits 8..23: the scene features
+// bit 0: the build lists sky items for another launch (DT_SKY_AGAIN); bit 1: it runs chunk items
+// (DT_CHUNK_ITEMS); bits 8..23: the scene features
 // it handles (DT_FEATURES; dt_api.cpp launches it only for scenes within them)
 extern "C" int DT_CAT(DT_TRACE_KERNEL, _traits)(void)
 {
-  return (DT_SKY_AGAIN ? 1 : 0) | (int)(((DT_FEATURES) & 0xFFFFu) << 8);
+  return (DT_SKY_AGAIN ? 1 : 0) | (DT_CHUNK_ITEMS ? 2 : 0) | (int)(((DT_FEATURES) & 0xFFFFu) << 8);
 }
 #endif
 #endif   // !DT_REPRO

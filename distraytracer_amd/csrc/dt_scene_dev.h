@@ -195,10 +195,11 @@ struct DParams {
   int32_t sgb_bx, sgb_by, sgb_nbx, sgb_nby;
   int32_t sgb_multi;      // a wave walks the subtrees of up to this many blocks in turn (DT_SG_SUB_MULTI)
   int32_t sgb_bz;         // the blocks' depth in cells (z; DT_SG_SUB_BLOCK XxYxZ)
-  // dt_render_repeat_async: n_frames copies of the frame's items in one launch, copy f storing into
-  // out + f * frame_stride floats (1: one frame, the default)
-  int32_t n_frames;
-  int64_t frame_stride;
+  // spp > 64: 1 = each 64-sample chunk of a pixel is a queue item of its own (code = pixel item *
+  // chunks + chunk), so a pixel's chunks run on different waves; the chunk that completes the pixel
+  // adds every sample colour in sample order (dt_kernels.hip item loop). 2 = the same with the queue
+  // chunk-major (code = chunk * n_items + pixel item: a pixel's chunks far apart; the tests' check)
+  int32_t chunk_items;
 };
 
 #ifndef DT_HD

@@ -411,8 +411,6 @@ int fill_params(const dt_globals& g, int frame, const dt_tiles* tiles, DParams& 
   memset(&P, 0, sizeof(P));
   for (int l = 0; l < DT_MAX_SGRID; ++l) P.sgb_base[l] = -1;   // no block subtrees (the scene sets them)
   P.sgb_bz = 1;
-  P.n_frames = 1;
-  P.frame_stride = 0;
   if (g.xRes <= 0 || g.yRes <= 0 || g.antialias_samples < 1 || g.max_depth < 0 || g.brdf_samples < 0 ||
       g.blur_samples < 0) {
     err = "invalid globals";

@@ -26,7 +26,9 @@ def tile_side(world, spp=64):
     (profiles/r05zl_rank_balance_c4_tiles.log)."""
     if world <= 1:
         return 32
-    return 16 if spp > 64 else 8
+    # the samples the kernel takes: int(sqrt(aa))^2 (host_flatten.cpp; aa = 65..80 is one chunk)
+    import math
+    return 16 if int(math.isqrt(max(int(spp), 1))) ** 2 > 64 else 8
 
 
 class FrameSplit:
@@ -134,18 +136,21 @@ class FrameQueue:
 
     frames: the frame ids to render; cost: {frame id: estimated cost} (missing ids: the mean);
     store: a torch.distributed Store (None: a single process, plain iteration); key, epoch: the
-    store keys of this queue, the same on every rank (a second pass or a retry in the same process
-    group passes another epoch, so its counter starts at 0); rank, world: this process's place in
-    the group (default: torch.distributed's)."""
+    store keys of this queue, the same on every rank. With a store the epoch is required: a second
+    queue in the same process group must pass another one, so that its counter starts at 0 (a queue
+    whose keys are already in the store is refused, on every rank); rank, world: this process's
+    place in the group (default: torch.distributed's)."""
 
-    def __init__(self, frames, cost=None, store=None, key="dt_frame_queue", epoch=0, rank=None, world=None):
+    def __init__(self, frames, cost=None, store=None, key="dt_frame_queue", epoch=None, rank=None, world=None):
         cost = cost or {}
         known = [cost[n] for n in frames if n in cost]
         mean = sum(known) / len(known) if known else 1.0
         # stable: equal costs keep the frames' own order
         self.order = sorted(frames, key=lambda n: -cost.get(n, mean))
         self.store = store
-        self.key = "%s/%d" % (key, epoch)
+        if store is not None and epoch is None:
+            raise ValueError("FrameQueue: pass an epoch with a store (one per queue in the process group)")
+        self.key = "%s/%d" % (key, epoch or 0)
         self._local = 0
         if store is not None:
             if rank is None or world is None:
@@ -157,7 +162,13 @@ class FrameQueue:
             # so on a mismatch every rank raises (none goes on rendering)
             import hashlib
             h = hashlib.sha1(repr(self.order).encode()).hexdigest()
-            store.set("%s/order/%d" % (self.key, rank), h)
+            # a reused epoch: its counter is already past frames, or a rank's order hash is stale. The
+            # check comes before this rank publishes its own hash, and no rank hands out a frame
+            # before every hash is published, so no rank of this queue can have created these keys
+            used = store.check([self.key]) or store.check(["%s/order/%d" % (self.key, rank)])
+            store.set("%s/order/%d" % (self.key, rank), "used" if used else h)
+            if used:
+                raise RuntimeError("FrameQueue %s: the store already holds this queue's keys (pass a new epoch)" % self.key)
             keys = ["%s/order/%d" % (self.key, r) for r in range(world)]
             store.wait(keys)
             hashes = [store.get(k) for k in keys]

@@ -43,7 +43,9 @@ extern "C" {
 /* 4: dt_scene_set_kernel (the trace-kernel choice per scene, not through the environment) */
 /* 5: dt_accel_info.features */
 /* 6: dt_trace_build (the trace-kernel build a render launches, and the features it covers) */
-#define DT_ABI_VERSION 7
+/* 7: dt_render_repeat_async; dt_accel_info.sg_sub_blocks / sg_sub_nodes / sg_sub_hash */
+/* 8: dt_render_repeat_async removed (a measurement stand-in with no product caller) */
+#define DT_ABI_VERSION 8
 
 /* ---- status codes ------------------------------------------------------- */
 #define DT_OK              0
@@ -342,15 +344,6 @@ int dt_render(const dt_scene* s, const dt_globals* g, int32_t frame, const dt_ti
  * their kernels. dt_collect_stats reports the scene's last launch. */
 int dt_render_async(const dt_scene* s, const dt_globals* g, int32_t frame, const dt_tiles* tiles,
                     float* out_device, void* stream);
-/* The same frame n_frames times in ONE launch (ABI 7): the launch's queue runs over n_frames copies
- * of the frame's items back to back, copy f writing out_device + f * frame_stride floats (same
- * layout as dt_render_async; frame_stride 0 overwrites one output). The copies share one launch
- * and one drain of the persistent grid, which a launch per frame pays each time (at
- * C3's 1/8 share ~0.29 ms per frame). The counters dt_collect_stats reports are the sum over the
- * copies. Not for 1-spp sky frames (deferred sky). No reference counterpart: the reference renders
- * one frame per process (render_final_project.cpp:965-1222). */
-int dt_render_repeat_async(const dt_scene* s, const dt_globals* g, int32_t frame, const dt_tiles* tiles,
-                           float* out_device, int32_t n_frames, int64_t frame_stride, void* stream);
 int dt_collect_stats(const dt_scene* s, void* stream, dt_stats* stats);
 
 /* diagnostic builds (-DDT_STAMPS): per-phase cycle sums of the last render; zeros otherwise */

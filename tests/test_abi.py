@@ -31,7 +31,7 @@ def test_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert dt.lib.dt_abi_version() == 7 == _lib.ABI_VERSION
+    assert dt.lib.dt_abi_version() == 8 == _lib.ABI_VERSION
 
 
 STRUCTS = {"dt_globals": _lib.Globals, "dt_shape_desc": _lib.ShapeDesc, "dt_light_desc": _lib.LightDesc,

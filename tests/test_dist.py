@@ -143,11 +143,26 @@ def _queue_worker(rank, world, port, result_path):
             mismatch = True
         flags = [None] * world
         dist.all_gather_object(flags, mismatch)
+        # a queue built again on a used epoch is refused on every rank (its counter is past the end:
+        # it would hand out nothing), and a store without an epoch is refused outright
+        dist.barrier()
+        try:
+            FrameQueue(frames, cost, store, epoch=0, rank=rank, world=world)
+            reused = False
+        except RuntimeError:
+            reused = True
+        try:
+            FrameQueue(frames, cost, store, rank=rank, world=world)
+            no_epoch = False
+        except ValueError:
+            no_epoch = True
+        refused = [None] * world
+        dist.all_gather_object(refused, [reused, no_epoch])
         if rank == 0:
             with open(result_path, "w") as f:
                 import json
                 json.dump({"per_rank": [e[0] for e in everyone], "second": [e[1] for e in everyone],
-                           "order": q.order, "mismatch": flags}, f)
+                           "order": q.order, "mismatch": flags, "refused": refused}, f)
     finally:
         dist.destroy_process_group()
 
@@ -170,6 +185,7 @@ def test_frame_queue_hands_out_every_frame_once(tmp_path):
     assert sorted(n for lst in r["second"] for n in lst) == list(range(5))
     # rank 1's order is the reverse of ranks 0 and 2's: every rank sees the disagreement and raises
     assert all(r["mismatch"])
+    assert all(a and b for a, b in r["refused"])   # a reused epoch, and a store without an epoch
 
 
 def test_frame_queue_single_process():

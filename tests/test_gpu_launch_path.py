@@ -86,50 +86,3 @@ def test_two_scenes_alternating_streams(cuda):
         st = dt.collect_stats(s)
         assert {k: getattr(st, k) for k in KEYS} == ref_st
         s.close()
-
-
-@pytest.mark.parametrize("built_frame,tiled", [(240, False), (240, True), (1440, False)])
-def test_repeat_launch_copies_equal_single_renders(cuda, built_frame, tiled):
-    """dt_render_repeat_async: n copies of the frame in one launch (one queue over the copies' items,
-    listed sky items carrying their copy) each equal the single render bit for bit; the counters
-    are the copies' sum."""
-    g, b = _globals(built_frame, (160, 96), 4)
-    tile = dt.tiles(tile_w=8, tile_h=8, rank=1, world=4, layout=dt.DT_OUT_SLAB) if tiled else None
-    ref, ref_st = _fresh(b, g, built_frame, tile)
-    n = 3
-    stride = ref.size
-    s = dt.Scene(b, g)
-    big = torch.full((stride * n,), -1.0, dtype=torch.float32, device="cuda")
-    dt.render_repeat_async(s, g, built_frame, big, n, stride, tile)
-    torch.cuda.synchronize()
-    st = dt.collect_stats(s)
-    s.close()
-    got = big.cpu().numpy().reshape(n, stride)
-    for f in range(n):
-        assert np.array_equal(got[f], ref), "copy %d" % f
-    assert st.rays == n * ref_st["rays"] and st.shadow_rays == n * ref_st["shadow_rays"]
-
-
-@pytest.mark.parametrize("aa", [4, 64])
-def test_repeat_launch_with_sky_items(cuda, aa):
-    """The still builds list the items with a missed sample for the *_sky build's second launch
-    (DT_SKY_AGAIN); in a repeat launch a listed item carries its copy. The spheres scene with
-    perlin_cloud on (sky around the spheres, tests/test_gpu_edges.py): three copies against one
-    render, 4-wave (4 spp) and 5-wave (64 spp) builds."""
-    g = dt.globals_default()
-    b = dt.build_scene("spheres", 0, g)
-    g.perlin_cloud = 1
-    g.xRes, g.yRes, g.antialias_samples, g.max_depth = 48, 32, aa, 2
-    ref, ref_st = _fresh(b, g, 0, None)
-    assert ref_st["sky_pixels"] > 0
-    n, stride = 3, ref.size
-    s = dt.Scene(b, g)
-    big = torch.full((stride * n,), -1.0, dtype=torch.float32, device="cuda")
-    dt.render_repeat_async(s, g, 0, big, n, stride, None)
-    torch.cuda.synchronize()
-    st = dt.collect_stats(s)
-    s.close()
-    got = big.cpu().numpy().reshape(n, stride)
-    for f in range(n):
-        assert np.array_equal(got[f], ref), "copy %d" % f
-    assert st.sky_pixels == n * ref_st["sky_pixels"] and st.rays == n * ref_st["rays"]

@@ -8,7 +8,6 @@ T_1 / (N * max_r T_r) bounds the kernel-side strong-scaling efficiency of bench.
     TILE_W=<w> TILE_H=<h>: non-square tiles at world > 1)
 
 RES=3840x2160: the config at another resolution. WORLDS=8 (or 1,8 ...): only these world sizes (the efficiency then needs world 1 among them).
-MULTI=n: each rank's time per frame of n copies of the frame in ONE launch (dt_render_repeat_async).
 INFLIGHT=n (2, 3, ...): each rank's time per frame over 16 frames rendered back to back on n streams with
 one scene object each (bench.py renders two in flight at N > 1), instead of one launch's kernel time.
 """
@@ -51,22 +50,6 @@ def main():
             ms = (time.perf_counter() - t0) * 1e3 / 16
             best = ms if best is None else min(best, ms)
         return best
-    def multi_ms(tile, out, n):
-        """wall time per frame of n copies of the frame in one launch (dt_render_repeat_async)"""
-        import time
-        slab = out.numel()
-        big = torch.zeros(slab * n, dtype=torch.float32, device="cuda")
-        dt.render_repeat_async(scene, g, 240, big, n, slab, tile)
-        torch.cuda.synchronize()
-        best = None
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            dt.render_repeat_async(scene, g, 240, big, n, slab, tile)
-            torch.cuda.synchronize()
-            ms = (time.perf_counter() - t0) * 1e3 / n
-            best = ms if best is None else min(best, ms)
-        return best
-    multi = int(os.environ.get("MULTI", "0"))
     from distraytracer_amd.multigpu import tile_side
     t1 = None
     worlds = [int(v) for v in os.environ.get("WORLDS", "1,2,4,8").split(",")]
@@ -80,9 +63,7 @@ def main():
             tile = dt.tiles(rank=rank, world=world, layout=dt.DT_OUT_SLAB, tile_w=tw, tile_h=th)
             out = torch.zeros(max(dt.slab_floats(g, tile), 1), dtype=torch.float32, device="cuda")
             st = dt.render(scene, g, 240, out, tile)   # warm-up
-            if multi >= 2:
-                best = multi_ms(tile, out, multi)
-            elif inflight >= 2:
+            if inflight >= 2:
                 best = frame_ms(tile, out)
             else:
                 best = min(dt.render(scene, g, 240, out, tile).kernel_ms for _ in range(reps))
