@@ -117,7 +117,7 @@ class AccelInfo(ctypes.Structure):
 EXPORTS = ["dt_abi_version", "dt_last_error", "dt_globals_default", "dt_scene_create", "dt_scene_destroy",
            "dt_scene_prepare", "dt_scene_upload", "dt_scene_set_kernel",
            "dt_scene_bvh", "dt_bvh_build", "dt_accel_info_build", "dt_trace_build", "dt_slab_floats", "dt_slab_floats_max",
-           "dt_render", "dt_render_async", "dt_collect_stats", "dt_debug_counters", "dt_render_sky",
+           "dt_render", "dt_render_async", "dt_collect_stats", "dt_debug_counters", "dt_debug_item_costs", "dt_render_sky",
            "dt_unpack_slabs", "dt_build_scene", "dt_scene_desc_free", "dt_write_ppm", "dt_write_png",
            "dt_mocap_bone_table", "dt_debug_normalize", "dt_intersect_primary",
            "dt_debug_load_obj"]
@@ -174,6 +174,7 @@ def _load():
                                       ctypes.c_void_p]),
         "dt_collect_stats": (c_int32, [ctypes.c_void_p, ctypes.c_void_p, P(Stats)]),
         "dt_debug_counters": (c_int32, [ctypes.c_void_p, P(c_uint64), c_int32]),
+        "dt_debug_item_costs": (c_int64, [ctypes.c_void_p, P(ctypes.c_uint32), c_int64]),
         "dt_debug_normalize": (c_int32, [P(c_double), P(c_double), c_int64]),
         "dt_render_sky": (c_int32, [P(Globals), c_float, P(Tiles), ctypes.c_void_p, c_int32, ctypes.c_void_p,
                                     P(Stats)]),
@@ -191,6 +192,9 @@ def _load():
                                           P(c_double), P(c_int32), P(c_int32)]),
     }
     for name, (res, args) in sig.items():
+        # a variant library built from an older tree for an A/B (DT_LIB) may lack a newer debug hook
+        if name.startswith("dt_debug_") and os.environ.get("DT_LIB") and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

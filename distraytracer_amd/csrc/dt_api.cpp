@@ -23,6 +23,7 @@ extern "C" size_t dt_scene_struct_size(void);
 extern "C" size_t dt_params_struct_offset(void);
 extern "C" hipError_t dt_launch_sky(const void* dev_launch, float* out, int64_t n_threads, hipStream_t stream);
 extern "C" hipError_t dt_launch_sky_miss(const void* dev_launch, float* out, int64_t n_px, hipStream_t stream);
+extern "C" hipError_t dt_launch_chunk_sum(const void* dev_launch, float* out, int64_t n_px, hipStream_t stream);
 extern "C" hipError_t dt_launch_unpack(const void* dev_launch, int world, int64_t slab_floats, const float* slabs,
                                        float* image, hipStream_t stream);
 extern "C" hipError_t dt_launch_normalize(const double* in, double* out, int64_t n, hipStream_t stream);
@@ -82,8 +83,9 @@ struct HScene {
   unsigned long long* clear0;   // the other parity's counters, zeroed by the launch (dt_kernels.hip)
   unsigned long long* clear1;
   int32_t n_clear0, n_clear1;
-  double* chunk_cols;           // chunk items: per-pixel sample colours and arrival words (dt_kernels.hip)
-  unsigned int* chunk_arrive;
+  double* chunk_cols;           // chunk items: per-pixel sample colours (dt_kernels.hip)
+  uint32_t* item_cost;          // diagnostic builds: per-item durations (dt_debug_item_costs)
+  void* pad_;
 };
 
 // DT_N_STAMPS (dt_scene_dev.h): diagnostic counter slots of -DDT_STAMPS builds (dt_debug_counters):
@@ -224,9 +226,10 @@ struct dt_scene {
   bool again_used = false;                  // the last render ran the second launch
   void* d_dn_pool = nullptr;       // dt_trace_kernel_dn: DT_DN_POOL_REC work-sharing records per wave
   int64_t dn_pool_waves = 0;
-  double* d_chunk_cols = nullptr;          // chunk items: spp sample colours per pixel item
-  unsigned int* d_chunk_arrive = nullptr;  // ... and one arrival word per pixel item (kept zero between launches)
-  int64_t chunk_cols_cap = 0, chunk_arrive_cap = 0;
+  double* d_chunk_cols = nullptr;   // chunk items: spp sample colours per pixel item
+  int64_t chunk_cols_cap = 0;
+  uint32_t* d_item_cost = nullptr;  // DT_ITEM_COSTS=1 (diagnostic builds): per-item durations
+  int64_t item_cost_cap = 0, item_cost_n = 0;
   PrimLists pl;
   bool pl_ok = false;
   void* d_pl_cells = nullptr;
@@ -384,7 +387,7 @@ static void release_device(dt_scene* s)
                    &s->d_sg_cells, &s->d_sg_list, &s->d_sub_nodes, &s->d_sub_blocks, &s->d_leaf, &s->d_hdr, &s->d_geom, &s->d_mat, &s->d_lights,
                    &s->d_tex, &s->d_zs, (void**)&s->d_stats, &s->d_launch, (void**)&s->d_sky_miss, &s->d_dn_pool,
                    (void**)&s->d_again, &s->d_launch2, (void**)&s->d_stats2, (void**)&s->d_chunk_cols,
-                   (void**)&s->d_chunk_arrive};
+                   (void**)&s->d_item_cost};
   for (void** b : bufs) {
     if (*b) (void)hipFree(*b);
     *b = nullptr;
@@ -404,7 +407,8 @@ static void release_device(dt_scene* s)
   s->zs_cap = 0;
   s->sky_miss_cap = 0;
   s->dn_pool_waves = 0;
-  s->chunk_cols_cap = s->chunk_arrive_cap = 0;
+  s->chunk_cols_cap = 0;
+  s->item_cost_cap = s->item_cost_n = 0;
   s->copy_pending = s->timed = s->launched = false;
   s->pl_dirty = true;   // the primary lists go up again with the next upload
 }
@@ -868,36 +872,48 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   const int64_t waves = kb.resident;
   // Chunk items (spp > 64: C4's 256): every 64-sample chunk of a pixel is a queue item of its own, so
   // a pixel's chunks run on different waves and a long pixel no longer holds one wave for four
-  // chunks in turn; the chunk that completes a pixel adds its spp sample colours in sample order
-  // (dt_kernels.hip). DT_CHUNK_ITEMS=0 / 1 / 2 (2: the queue chunk-major) overrides the default.
+  // chunks in turn. The chunks store their sample colours; dt_chunk_sum_kernel adds each pixel's up
+  // in sample order after the trace launch(es) (dt_kernels.hip). For a rank's share of a split frame
+  // (world > 1): C4's world-8 shares 44.0 against 48.6 ms for the slowest (profiles/r06c_rb_*). A
+  // whole frame keeps one item per pixel: there the stored colours and the sum kernel cost C4 1.5%
+  // (1710 against 1736 Mpixel-samples/s with the chunks of a pixel dequeued together, r06b).
+  // DT_CHUNK_ITEMS=0 / 1 / 2 (2: the queue chunk-major, the tests' check) overrides the default.
   const char* ci_env = getenv("DT_CHUNK_ITEMS");
-  int chunk_items = ci_env ? atoi(ci_env) : 1;
+  int chunk_items = ci_env ? atoi(ci_env) : (P.world > 1 ? 1 : 0);
   // (the build and, for a sky-item launch, its *_sky build must carry the code: trait bit 1)
-  if (!(kb.traits() & 2) || !(kb2.traits() & 2) || P.chunks < 2 || P.chunks > 255 ||
-      chunk_items < 0 || chunk_items > 2 ||
-      (double)P.n_items * P.chunks >= 4294967296.0)
+  if (!(kb.traits() & 2) || !(kb2.traits() & 2) || P.chunks < 2 || P.chunks > 255 || chunk_items < 0 ||
+      chunk_items > 2 || (double)P.n_items * P.chunks >= 4294967296.0)
     chunk_items = 0;
   P.chunk_items = chunk_items;
   if (chunk_items) {
     const int64_t n_cols = P.n_items * (int64_t)P.spp * 3;
-    if (n_cols > sc->chunk_cols_cap || P.n_items > sc->chunk_arrive_cap) {
+    if (n_cols > sc->chunk_cols_cap) {
       HIPCHK(hipStreamSynchronize(st));
       if (sc->d_chunk_cols) (void)hipFree(sc->d_chunk_cols);
-      if (sc->d_chunk_arrive) (void)hipFree(sc->d_chunk_arrive);
       sc->d_chunk_cols = nullptr;
-      sc->d_chunk_arrive = nullptr;
-      sc->chunk_cols_cap = sc->chunk_arrive_cap = 0;
+      sc->chunk_cols_cap = 0;
       HIPCHK(hipMalloc((void**)&sc->d_chunk_cols, sizeof(double) * (size_t)n_cols));
-      HIPCHK(hipMalloc((void**)&sc->d_chunk_arrive, sizeof(unsigned int) * (size_t)P.n_items));
-      // zero once: the wave that completes a pixel zeroes its word again
-      HIPCHK(hipMemsetAsync(sc->d_chunk_arrive, 0, sizeof(unsigned int) * (size_t)P.n_items, st));
       sc->chunk_cols_cap = n_cols;
-      sc->chunk_arrive_cap = P.n_items;
     }
   }
   hs.chunk_cols = chunk_items ? sc->d_chunk_cols : nullptr;
-  hs.chunk_arrive = chunk_items ? sc->d_chunk_arrive : nullptr;
   const int64_t n_queue = P.n_items * (chunk_items ? P.chunks : 1);
+  // DT_ITEM_COSTS=1: every item's duration, for builds that record it (-DDT_ITEM_TIMES=2; others leave
+  // the array as it is): dt_debug_item_costs
+  hs.item_cost = nullptr;
+  if (getenv("DT_ITEM_COSTS") && getenv("DT_ITEM_COSTS")[0] == '1' && n_queue > 0) {
+    if (n_queue > sc->item_cost_cap) {
+      HIPCHK(hipStreamSynchronize(st));
+      if (sc->d_item_cost) (void)hipFree(sc->d_item_cost);
+      sc->d_item_cost = nullptr;
+      sc->item_cost_cap = 0;
+      HIPCHK(hipMalloc((void**)&sc->d_item_cost, sizeof(uint32_t) * (size_t)n_queue));
+      sc->item_cost_cap = n_queue;
+    }
+    HIPCHK(hipMemsetAsync(sc->d_item_cost, 0, sizeof(uint32_t) * (size_t)n_queue, st));
+    hs.item_cost = sc->d_item_cost;
+    sc->item_cost_n = n_queue;
+  }
   int64_t grid = n_queue < waves ? n_queue : waves;
   if (grid < 1) grid = 1;
   hs.dn_pool = nullptr;
@@ -933,11 +949,12 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   // for a rank's share of a split frame of one-chunk items: C3's world-8 shares 4.46 against 4.54 ms
   // (bound 0.933 against 0.921, profiles/r05zg_rank_balance_segs_default.log), C2's 0.569 against
   // 0.591. A whole frame keeps one counter (C3 -1.4%, C4 -3.4%, C2 -0.5% with eight), and so do
-  // multi-chunk items (C4's world-8 shares 49.4 against 47.1 ms with eight, profiles/r05zi_*).
-  // DT_QUEUE_SEGS=<n> (1..8) overrides.
+  // pixels of several chunks in one item (C4's world-8 shares 49.4 against 47.1 ms with eight,
+  // profiles/r05zi_*). Chunk items take eight: C4's slowest world-8 share 43.97 against 45.77 ms
+  // (profiles/r06c_rb_m1s8.log, r06c_rb_m1.log). DT_QUEUE_SEGS=<n> (1..8) overrides.
   const char* qs = getenv("DT_QUEUE_SEGS");
   PL.queue_segs = qs ? std::max(1, std::min(atoi(qs), DT_QSEG_MAX))
-                     : (PL.world > 1 && PL.chunks == 1 ? DT_QSEG_MAX : 1);
+                     : (PL.world > 1 && (PL.chunks == 1 || PL.chunk_items) ? DT_QSEG_MAX : 1);
   // deep-cascade waves raise their priority (dt_kernels.hip, DT_PRIO_STEPS) when the frame is split
   // over ranks, where one such wave bounds a rank's kernel; DT_PRIO_STEPS=<n> overrides (0: off)
   const char* ps = getenv("DT_PRIO_STEPS");
@@ -1069,6 +1086,8 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   }
   sc->again_used = again;
   if (PL.sky_defer) HIPCHK(dt_launch_sky_miss(d_rec, out_dev, n_px, st));
+  // chunk items: every pixel's sample colours added up in sample order, once both launches stored theirs
+  if (PL.chunk_items) HIPCHK(dt_launch_chunk_sum(d_rec, out_dev, PL.n_items, st));
   HIPCHK(hipEventRecord(sc->ev1, st));
   sc->timed = true;
   sc->launched = true;
@@ -1428,6 +1447,19 @@ extern "C" int dt_debug_counters(const dt_scene* sc, uint64_t* out, int32_t n)
                    hipMemcpyDeviceToHost));
   for (int i = 0; i < n; ++i) out[i] = h[ST_N + 1 + i];
   return DT_OK;
+}
+
+extern "C" int64_t dt_debug_item_costs(const dt_scene* sc, uint32_t* out, int64_t n)
+{
+  if (!sc || (n > 0 && !out) || n < 0) return (int64_t)fail(DT_E_INVALID, "bad arguments");
+  if (!sc->d_item_cost || sc->item_cost_n == 0) return 0;
+  const int64_t m = n < sc->item_cost_n ? n : sc->item_cost_n;
+  if (m > 0) {
+    if (hipDeviceSynchronize() != hipSuccess) return (int64_t)fail(DT_E_NO_DEVICE, "hipDeviceSynchronize");
+    if (hipMemcpy(out, sc->d_item_cost, sizeof(uint32_t) * (size_t)m, hipMemcpyDeviceToHost) != hipSuccess)
+      return (int64_t)fail(DT_E_NO_DEVICE, "hipMemcpy");
+  }
+  return sc->item_cost_n;
 }
 
 extern "C" int dt_debug_normalize(const double* in, double* out, int64_t n)

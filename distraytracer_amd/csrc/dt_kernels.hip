@@ -109,9 +109,10 @@ using namespace dtd;
 #define DT_SKY_AGAIN 0
 #endif
 #define DT_AGAIN_QUEUE DT_SKY_BUILD
-// DT_CHUNK_ITEMS=1: the build can run chunk items (P.chunk_items, spp > 64: a pixel's 64-sample chunks
-// on different waves). The room builds (C2, C3, C5's room frames: never more than 64 spp) leave the
-// code out (5-wave room build: +3 VGPR, +24 SGPR spills with it); dt_api.cpp reads the trait bit.
+// DT_CHUNK_ITEMS=1 (every build): the build can run chunk items (P.chunk_items, spp > 64: a pixel's
+// 64-sample chunks on different waves); dt_api.cpp reads the trait bit. A/B switch: the 5-wave room
+// build without the code ran C3 1.3% slower (register allocation: 3872 against 3920 Mpixel-samples/s,
+// profiles/r06d_*), so it stays in.
 #ifndef DT_CHUNK_ITEMS
 #define DT_CHUNK_ITEMS 1
 #endif
@@ -212,9 +213,12 @@ struct DScene {
   unsigned long long* clear1;
   int32_t n_clear0, n_clear1;
   // P.chunk_items (spp > 64): per pixel item, its spp sample colours (3 doubles each, sample order),
-  // published by the chunk items that traced them, and its arrival word (dt_trace kernel item loop)
+  // stored by the chunk items that traced them and added up by dt_chunk_sum_kernel
   double* chunk_cols;
-  unsigned int* chunk_arrive;
+  // diagnostic builds (-DDT_ITEM_TIMES=2, DT_ITEM_COSTS=1): per queue code, the item's duration on the
+  // 100 MHz clock (dt_debug_item_costs, tools/chunk_costs.py); null otherwise
+  uint32_t* item_cost;
+  void* pad_;   // (keeps sizeof(DScene) a multiple of 16: DLaunch::P at the offset it had)
 };
 
 // pow(x, n) for the integer exponents the reference writes as pow(x, 2.0) etc. pow(x, 1) is x
@@ -3120,7 +3124,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   const int batch = P.item_batch > 1 ? P.item_batch : 1;
   // P.sky_again == 2: the queue runs over the items a launch without the sky listed
   const int64_t n_queue = DT_AGAIN_QUEUE && P.sky_again == 2 ? (int64_t)*S.again_n
-                                                             : P.n_items * (P.chunk_items ? P.chunks : 1);
+                                                             : P.n_items * (DT_CHUNK_ITEMS && P.chunk_items ? P.chunks : 1);
   // P.queue_segs > 1: the queue in that many contiguous segments with a counter each; wave b starts
   // in segment b % segs (workgroups go round-robin to the XCDs) and takes its first batch there by
   // block index, then from the segment's counter; a drained segment sends the wave to the next one,
@@ -3177,7 +3181,7 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       chunk_lo = (int)ck;
       chunk_hi = chunk_lo + 1;
     }
-    bool px_done = true;   // chunk items: this chunk completed its pixel (it stores it)
+    bool px_done = true;   // false for chunk items: dt_chunk_sum_kernel stores their pixels
     bool sky_again = false;
 #if DT_AGAIN_QUEUE
     // the item's counters are taken back: the launch that listed it counted it already
@@ -3291,65 +3295,24 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       }
       DT_T(k2);
       DT_ACC(6, k1, k2);
-      // ordered per-pixel sum (cpp:1212: color += tmp_color in sample order). red takes this chunk's
-      // sample colours; for chunk items, once this chunk completed its pixel, the pixel's chunks in turn
-      int ck_lo = chunk, ck_hi = chunk + 1;
-      typedef __attribute__((address_space(1))) unsigned long long gu64;
-      typedef __attribute__((address_space(1))) unsigned int gu32;
       if (DT_CHUNK_ITEMS && P.chunk_items) {
-        // The chunk publishes its 64 sample colours in the pixel's slot and arrives on the pixel's
-        // word; the chunk that completes the pixel adds all spp colours in sample order, the same
-        // additions in the same order as one wave running the chunks in turn. Hand-off across
-        // workgroups and XCDs: write-through (sc1) stores, every lane's stores drained before the
-        // agent-scope arrival; the completing wave acquires at agent scope before its plain loads.
-        // Arrival word: bits 0-15 chunks arrived, 16-23 chunks listed for the sky launch
-        // (P.sky_again 1), 24-31 listed chunks arrived in that launch (P.sky_again 2). The wave
-        // that completes the pixel zeroes the word for the next launch.
-        gu64* const slot = (gu64*)(S.chunk_cols + ((int64_t)item * spp + chunk * DT_WAVE + lane) * 3);
+        // chunk items: the chunk stores its sample colours in its pixel's slot, in sample order
+        // (coalesced: 64 lanes x 24 B); dt_chunk_sum_kernel adds each pixel's colours up after the
+        // launch (dt_api.cpp), so no item of this launch stores a pixel
+        double* const slot = S.chunk_cols + ((int64_t)item * spp + chunk * DT_WAVE + lane) * 3;
         if (valid) {
-          __hip_atomic_store(slot, (unsigned long long)__double_as_longlong(tmp_color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(slot + 1, (unsigned long long)__double_as_longlong(tmp_color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(slot + 2, (unsigned long long)__double_as_longlong(tmp_color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          slot[0] = tmp_color.x;
+          slot[1] = tmp_color.y;
+          slot[2] = tmp_color.z;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        px_done = false;
+      } else {
+        // ordered per-pixel sum (cpp:1212: color += tmp_color in sample order)
+        red[lane * 3 + 0] = tmp_color.x;
+        red[lane * 3 + 1] = tmp_color.y;
+        red[lane * 3 + 2] = tmp_color.z;
         __syncthreads();
-        const uint32_t add1 = P.sky_again == 2 ? (1u << 24) : 1u + (sky_again ? (1u << 16) : 0u);
-        if (lane == 0)
-          item_s = __hip_atomic_fetch_add((gu32*)(S.chunk_arrive + item), add1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const uint32_t w = (uint32_t)item_s + add1;
-        px_done = P.sky_again == 2 ? (w >> 24) == ((w >> 16) & 0xFFu)
-                                   : (w & 0xFFFFu) == (uint32_t)P.chunks && (w >> 16) == 0;
-        __syncthreads();
-        ck_lo = 0;
-        ck_hi = px_done ? P.chunks : 0;
-        if (px_done) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();
-        }
-      }
-#if DT_CHUNK_ITEMS
-      for (int ck = ck_lo; ck < ck_hi; ++ck) {
-#else
-      {   // (a loop of one trip would stay a loop: -fno-unroll-loops)
-        const int ck = chunk;
-        (void)ck_lo; (void)ck_hi;
-#endif
-        if (DT_CHUNK_ITEMS && P.chunk_items) {
-          const double* const src = S.chunk_cols + ((int64_t)item * spp + ck * DT_WAVE + lane) * 3;
-          if (ck * DT_WAVE + lane < spp) {
-            red[lane * 3 + 0] = src[0];
-            red[lane * 3 + 1] = src[1];
-            red[lane * 3 + 2] = src[2];
-          }
-        } else {
-          red[lane * 3 + 0] = tmp_color.x;
-          red[lane * 3 + 1] = tmp_color.y;
-          red[lane * 3 + 2] = tmp_color.z;
-        }
-        __syncthreads();
-        int ns = spp - ck * DT_WAVE;
+        int ns = spp - chunk * DT_WAVE;
         if (ns > per) ns = per;
         if (group * 3 <= DT_WAVE) {
           // lane 3 jj + ch sums channel ch of pixel jj: the three channels' chains run side by side
@@ -3368,8 +3331,6 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
         }
         __syncthreads();
       }
-      if (DT_CHUNK_ITEMS && P.chunk_items && px_done && lane == 0)
-        __hip_atomic_store((gu32*)(S.chunk_arrive + item), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     DT_T(k3);
     const bool item_again = sky_again;
@@ -3411,6 +3372,9 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
 #endif
 #if DT_SKY_AGAIN
     if (item_again && lane == 0) S.again_list[atomicAdd(S.again_n, 1u)] = (uint32_t)code;
+#endif
+#if DT_ITEM_TIMES == 2
+    if (S.item_cost && lane == 0) S.item_cost[code] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - item_t0);
 #endif
     if (P.prio_steps > 0) __builtin_amdgcn_s_setprio(0);
     ++qpos;
@@ -3481,6 +3445,35 @@ dt_sky_miss_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   }
   const unsigned long long n = __popcll(__ballot(mine));
   if ((threadIdx.x & 63) == 0 && n) atomicAdd(S.stats + ST_SKY, n);
+}
+
+// Chunk items (P.chunk_items, spp > 64): every pixel's spp sample colours, stored by its chunk items
+// in sample order, added up in that order (cpp:1212: color += tmp_color; the same chain as the
+// per-pixel items' sums in LDS), then / spp (cpp:1213) and clamp*255 (store_pixel). One pixel per
+// thread, the three channels' chains side by side (add() is componentwise).
+extern "C" __global__ void __launch_bounds__(256)
+dt_chunk_sum_kernel(const DLaunch* __restrict__ Lp, float* __restrict__ out)
+{
+  const DParams& P = Lp->P;
+  const DScene& S = Lp->S;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool nan = false;
+  if (q < P.n_items) {
+    int x, y;
+    int64_t so;
+    bool valid;
+    pixel_of(P, q, x, y, so, valid);
+    if (valid) {
+      const double* __restrict__ c = S.chunk_cols + q * P.spp * 3;
+      V3 ps = v3(0, 0, 0);
+      for (int s = 0; s < P.spp; ++s) ps = add(ps, v3(c[3 * s], c[3 * s + 1], c[3 * s + 2]));
+      const V3 color = divs(ps, P.spp);
+      store_pixel(P, out, x, y, so, color);
+      nan = isnan(color.x) || isnan(color.y) || isnan(color.z);
+    }
+  }
+  const unsigned long long n = __popcll(__ballot(nan));
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(S.stats + ST_NAN, n);
 }
 
 // renderImageCloud (cpp:1224-1279): one pixel per lane
@@ -3566,6 +3559,12 @@ extern "C" hipError_t dt_launch_sky_miss(const void* dev_launch, float* out, int
 {
   int64_t blocks = (n_px + 255) / 256;
   hipLaunchKernelGGL(dt_sky_miss_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const DLaunch*)dev_launch, out);
+  return hipGetLastError();
+}
+extern "C" hipError_t dt_launch_chunk_sum(const void* dev_launch, float* out, int64_t n_px, hipStream_t stream)
+{
+  int64_t blocks = (n_px + 255) / 256;
+  hipLaunchKernelGGL(dt_chunk_sum_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const DLaunch*)dev_launch, out);
   return hipGetLastError();
 }
 extern "C" hipError_t dt_launch_sky(const void* dev_launch, float* out, int64_t n_threads, hipStream_t stream)

@@ -348,6 +348,10 @@ int dt_collect_stats(const dt_scene* s, void* stream, dt_stats* stats);
 
 /* diagnostic builds (-DDT_STAMPS): per-phase cycle sums of the last render; zeros otherwise */
 int dt_debug_counters(const dt_scene* s, uint64_t* out, int32_t n);
+/* diagnostic builds (-DDT_ITEM_TIMES=2) with DT_ITEM_COSTS=1 in the environment: the last launch's
+ * per-item durations (100 MHz clock ticks) by queue code (chunk items: pixel item * chunks + chunk),
+ * min(n, items) of them into out; returns the number of items (0: none recorded; < 0: an error code) */
+int64_t dt_debug_item_costs(const dt_scene* s, uint32_t* out, int64_t n);
 /* numerics check: the device kernels' normalisation of n VEC3s (Eigen normalized(), dt_math.h),
  * host arrays of 3n doubles; synchronous */
 int dt_debug_normalize(const double* in, double* out, int64_t n);

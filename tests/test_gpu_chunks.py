@@ -102,7 +102,8 @@ def test_chunk_items_sky_launch(cuda, monkeypatch, aa, world):
     built = dt.build_scene("spheres", 0, g)
     g.perlin_cloud = 1
     g.xRes, g.yRes, g.antialias_samples, g.max_depth = 40, 24, aa, 3
-    tile = dt.tiles(rank=world - 1, world=world, layout=dt.DT_OUT_SLAB) if world > 1 else dt.tiles()
+    tile = (dt.tiles(tile_w=8, tile_h=8, rank=world - 1, world=world, layout=dt.DT_OUT_SLAB) if world > 1
+            else dt.tiles())
     st, rst = _modes(monkeypatch, built, g, 0, tile, "spheres sky aa=%d world=%d" % (aa, world), repeat=2)
     assert rst.sky_pixels > 0 and st.sky_pixels > 0
 
