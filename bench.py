@@ -237,8 +237,9 @@ def main():
     ap.add_argument("--cpu-all-cores", action="store_true",
                     help="also time the CPU baseline on every core of the affinity mask (not the GPU box's default)")
     ap.add_argument("--no-roofline", action="store_true", help="skip the VALU work count (child process)")
-    ap.add_argument("--inflight", type=int, default=2, choices=(1, 2),
-                    help="N > 1 (torchrun): frames in flight per rank (2: alternating streams, DESIGN.md §7)")
+    ap.add_argument("--inflight", type=int, default=None, choices=(1, 2),
+                    help="frames in flight per rank (2, the default: alternating streams and scene objects, "
+                         "DESIGN.md §7)")
     args = ap.parse_args()
 
     import torch
@@ -268,15 +269,22 @@ def main():
     W, H = g.xRes, g.yRes
     spp = int(int(g.antialias_samples ** 0.5) ** 2)
     dev = torch.device("cuda", local)
+    # two frames in flight at every N: frame k+1's waves start on the CUs frame k's longest items leave
+    # idle. N = 1: C2 +3.3% (its kernel is bounded by a column of 30x-mean items, a glossy cascade of
+    # 6.6 rays per sample), C3 and C4 +-0.1% (profiles/r06j_*)
+    inflight = args.inflight or 2
     if not distributed:
-        image = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
+        # N = 1: with two frames in flight, frame k renders into images[k % 2] on streams[k % 2]
+        images = [torch.zeros(3 * W * H, dtype=torch.float32, device=dev) for _ in range(inflight)]
+        image = images[0]
+        streams1 = [torch.cuda.Stream(dev) for _ in range(2)] if inflight == 2 else None
         tile = dt.tiles()
     else:
         # double-buffered slabs: frame k's gather (RCCL, async) overlaps frame k+1's render
         # with two frames in flight, frame k renders on streams[k % 2] with a scene object of its own
         # (its own launch record and queue word): frame k+1's waves fill the CUs frame k's tail
         # leaves idle (C3's 1/8 share: -2.1% per frame, profiles/r03ap_philox_mad64_overlap.log)
-        streams = [torch.cuda.Stream(dev) for _ in range(2)] if args.inflight == 2 else None
+        streams = [torch.cuda.Stream(dev) for _ in range(2)] if inflight == 2 else None
         pipe = GatherPipeline(split, [torch.zeros(split.slab_floats, dtype=torch.float32, device=dev)
                                       for _ in range(2)],
                               [torch.zeros(world * split.slab_floats if rank == 0 else 1, dtype=torch.float32,
@@ -284,7 +292,7 @@ def main():
                               torch.zeros(3 * W * H if rank == 0 else 1, dtype=torch.float32, device=dev),
                               streams=streams)
         tile = split.tile
-    scenes = [scene, dt.Scene(built, g)] if distributed and args.inflight == 2 else [scene]
+    scenes = [scene, dt.Scene(built, g)] if inflight == 2 else [scene]
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
 
@@ -293,8 +301,8 @@ def main():
             pipe.finish()
 
     def step(k, evs=None):
-        out = image if not distributed else pipe.slab(k)
-        rs = (pipe.stream(k) if distributed else None) or stream
+        out = images[k % len(images)] if not distributed else pipe.slab(k)
+        rs = (pipe.stream(k) if distributed else (streams1[k % 2] if streams1 else None)) or stream
         if distributed:
             pipe.begin(k)
         if evs is not None:
@@ -306,7 +314,7 @@ def main():
             pipe.submit(k)
 
     for sc in scenes[1:]:   # setup of the second frame-in-flight scene: its first launch, untimed
-        dt.render(sc, g, 240, pipe.slab(1), tile)
+        dt.render(sc, g, 240, pipe.slab(1) if distributed else images[1], tile)
     for k in range(args.warmup):
         step(k)
     finish_pending()
@@ -407,7 +415,7 @@ def main():
                        "name": args.config, "use_model": int(g.use_model),
                        "frame": 240, "xRes": W, "yRes": H, "spp": spp, "max_depth": g.max_depth,
                        "parallelism": ("tile-split x%d + RCCL gather, %d frame(s) in flight" % (world, len(scenes))
-                                       if distributed else "single GPU")},
+                                       if distributed else "single GPU, %d frame(s) in flight" % len(scenes))},
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,

@@ -5,7 +5,7 @@ consecutive tiles (raster order), the ranks rotated by a hash of the group (dt_s
 tile_of), into a packed slab: the expensive sky/glossy regions spread over all GPUs, and unlike a
 plain t % world interleave no rank is tied to a fixed set of tile columns. The tile side follows
 the world size (tile_side): 8x8 (the primary lists' block) at every N > 1, where many tiles per
-rank even out the ranks' work, and 16x16 for pixels of several 64-sample chunks (spp > 64, C4). Rank-balance kernel times of C3 (profiles/r04zs_rank_balance_tiles.log,
+rank even out the ranks' work, and 2x2 for pixels of several 64-sample chunks (spp > 64, C4). Rank-balance kernel times of C3 (profiles/r04zs_rank_balance_tiles.log,
 slowest share 8x8 against 16x16): N=2 17.60 against 17.75 ms, N=4 9.09 against 9.12, N=8 4.73
 against 4.87 (round 3: slowest rank 6.29 -> 5.96 ms from 32x32, profiles/r03z_rank_balance_tiles.log).
 32x32 at N = 1, where the waves that run at once cover a compact part of the image: at world 1 the
@@ -21,14 +21,18 @@ from . import DT_OUT_SLAB, slab_floats_max, tiles, unpack_slabs
 
 def tile_side(world, spp=64):
     """the split's tile side for a world size and samples per pixel (module docstring). Pixels of
-    several 64-sample chunks (spp > 64) take 16x16 at N > 1: C4's bound 0.980 / 0.944 / 0.790 at
-    N = 2 / 4 / 8 against 0.970 / 0.939 / 0.764 with 8x8, twice each
-    (profiles/r05zl_rank_balance_c4_tiles.log)."""
+    several 64-sample chunks (spp > 64: C4) take 2x2 at N > 1, where each chunk is a queue item of
+    its own (chunk items, dt_api.cpp): C4's kernel-side bound 0.988 / 0.982 / 0.969 at N = 2 / 4 / 8
+    (every world-8 share within 39.2-39.6 ms; profiles/r06h_rb_c4_t2.log, r06i_rb_c4_t2.log), against
+    0.985 / 0.978 / 0.930 with 4x4, 0.986 / 0.956 / 0.915 with 8x8 and 0.974 / 0.980 / 0.871 with
+    16x16 (profiles/r06g_rb_t4.log, r06g_rb_t8.log, r06g_rb_t16.log). The cost is concentrated: the
+    longest 1% of C4's chunk items hold ~47% of the wave time, in a few clusters of mesh pixels
+    (profiles/r06e_costs_c4_w8.log), and small tiles spread each cluster over every rank."""
     if world <= 1:
         return 32
     # the samples the kernel takes: int(sqrt(aa))^2 (host_flatten.cpp; aa = 65..80 is one chunk)
     import math
-    return 16 if int(math.isqrt(max(int(spp), 1))) ** 2 > 64 else 8
+    return 2 if int(math.isqrt(max(int(spp), 1))) ** 2 > 64 else 8
 
 
 class FrameSplit:

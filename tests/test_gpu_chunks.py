@@ -67,7 +67,7 @@ def _modes(monkeypatch, built, g, frame, tile, label, modes=("1", "2", "0"), rep
 
 def test_c4_chunk_items(cuda, monkeypatch):
     """C4 (buildFinal(240) with the models, 1920x1080, 256 spp, depth 8), rank 5's share of a
-    256-way split in 16x16 tiles (multigpu.FrameSplit's tiles for spp > 64): chunk items pixel-major
+    256-way split in 16x16 tiles: chunk items pixel-major
     and chunk-major, and per-pixel items, bit-identical to each other and to the oracle."""
     g = dt.globals_default()
     g.use_model = 1

@@ -57,6 +57,7 @@ def main():
     ts = tile_side(world, g.antialias_samples)
     spp = int(int(g.antialias_samples ** 0.5) ** 2)
     chunks = (spp + 63) // 64
+    ppw = 64 // spp if spp <= 64 else 1   # pixels per wave item (dt_render: spp < 64 packs pixels)
     tiles_x = (g.xRes + ts - 1) // ts
     slots = int(os.environ.get("SLOTS", "5120"))
     for rank in ranks:
@@ -70,12 +71,12 @@ def main():
         c = np.zeros(n, dtype=np.uint32)
         dt.lib.dt_debug_item_costs(s.handle, c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n)
         ms = c.astype(np.float64) * 1e-5   # 100 MHz ticks -> ms
-        per_chunk = n != st.pixels and n % chunks == 0
+        per_chunk = chunks > 1 and n % chunks == 0 and n // chunks * ppw >= st.pixels
         order = np.argsort(ms)[::-1]
         top = []
         for code in order[:12]:
             item, ck = divmod(int(code), chunks) if per_chunk else (int(code), -1)
-            x, y = pixel_of(item, ts, ts, tiles_x, rank, world)
+            x, y = pixel_of(item * ppw, ts, ts, tiles_x, rank, world)   # (the item's first pixel)
             top.append({"x": x, "y": y, "chunk": ck, "ms": round(float(ms[code]), 3)})
         tot = ms.sum()
         srt = np.sort(ms)[::-1]
