@@ -4,9 +4,10 @@ Workload (BASELINE.json configs[2], north_star's target): buildFinal(240) — th
 scene (`./render` = frame 30 -> buildFinal(240)) without the missing OBJ models — at
 1920x1080, antialias_samples=64 (64 spp), max_depth=8, brdf_samples=2, aperture 0.2 (DoF),
 glossy floor/doors/cylinder, Cook-Torrance doors, 4 rectangle area lights + window point light.
-One step = one full frame. At N>1 the frame is tile-split over the ranks (32x32 tiles,
-round-robin) and the finished tiles are gathered to rank 0 over RCCL (strong scaling: the
-total work per step is one frame at every N).
+One step = one full frame; two frames are in flight on alternating streams (--inflight). At N>1
+the frame is tile-split over the ranks (multigpu.FrameSplit: hashed groups of 8x8 tiles, 2x2 for
+pixels of several 64-sample chunks) and the finished slabs are gathered to rank 0 over RCCL (strong
+scaling: the total work per step is one frame at every N).
 
 value = W*H*spp*steps / max-over-ranks wall time of the timed region (scene resident on the
 GPU, output in HBM; no host transfers inside).

@@ -95,7 +95,7 @@ enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SKY = 2, ST_UV = 3, ST_GLOSSY = 4, ST_SPHL
        ST_DONATE = 16, ST_DN_OVF = 17, ST_N = 18 };
 // one parity's counter block: the trace launch's (counters, queue word, stamps slots, segment
 // counters), the sky-item launch's (counters, queue word, list count)
-constexpr size_t STATS1 = ST_N + DT_QSEG_OFF + DT_QSEG_MAX * DT_QSEG_STRIDE, STATS2 = ST_N + 2;
+constexpr size_t STATS1 = ST_N + DT_STAT_SLOT_OFF + (DT_STAT_SLOTS - 1) * DT_STAT_SLOT_STRIDE, STATS2 = ST_N + 2;
 
 int fail(int code, const std::string& msg)
 {
@@ -1104,7 +1104,15 @@ int dt_collect_stats(const dt_scene* sc_c, void* stream, dt_stats* stats)
   HIPCHK(hipStreamSynchronize(st));
   if (!stats) return DT_OK;
   unsigned long long h[ST_N];
-  HIPCHK(hipMemcpy(h, sc->d_stats + sc->last_parity * STATS1, sizeof(h), hipMemcpyDeviceToHost));
+  {   // the counters and their per-slot copies (dt_kernels.hip: wave b adds to copy b % DT_STAT_SLOTS)
+    std::vector<unsigned long long> blk(STATS1);
+    HIPCHK(hipMemcpy(blk.data(), sc->d_stats + sc->last_parity * STATS1, sizeof(unsigned long long) * STATS1,
+                     hipMemcpyDeviceToHost));
+    for (int k = 0; k < ST_N; ++k) {
+      h[k] = blk[k];
+      for (int s = 1; s < DT_STAT_SLOTS; ++s) h[k] += blk[ST_N + DT_STAT_SLOT_OFF + (s - 1) * DT_STAT_SLOT_STRIDE + k];
+    }
+  }
   if (sc->again_used) {   // the listed items' second launch (dt_kernels.hip DT_SKY_AGAIN)
     unsigned long long h2[ST_N];
     HIPCHK(hipMemcpy(h2, sc->d_stats2 + sc->last_parity * STATS2, sizeof(h2), hipMemcpyDeviceToHost));

@@ -3381,7 +3381,6 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
   }
   {
     __syncthreads();
-    const unsigned long long r = wc_lds[WC_RAYS], sh = wc_lds[WC_SHADOW], tx = wc_lds[WC_TEX];
 #ifdef DT_WORK_COUNTERS
     __syncthreads();
     if (lane < DT_WK_N && wk_lds[lane]) atomicAdd(S.stats + ST_N + 1 + lane, (unsigned long long)wk_lds[lane]);
@@ -3392,19 +3391,25 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
       atomicAdd(S.stats + ST_PRIM, pr);
     }
 #endif
-    if (lane == 0) {
-      atomicAdd(S.stats + ST_WNODES, (unsigned long long)cnt.wnodes);
 #ifdef DT_STAMPS
+    if (lane == 0)
       for (int k = 0; k < DT_PH_N; ++k) atomicAdd(S.stats + ST_N + 1 + k, cnt.ph[k]);
 #endif
-      if (sky_px) atomicAdd(S.stats + ST_SKY, sky_px);
-      atomicAdd(S.stats + ST_RAYS, r);
-      atomicAdd(S.stats + ST_SHADOW, sh);
-      atomicAdd(S.stats + ST_TEX, tx);
-      const int st_of[WC_N] = {-1, -1, -1, ST_STACK, ST_REFL, ST_GLOSSY, ST_UV, ST_PRISM, ST_SPHL};
-      for (int k = WC_STACK; k < WC_N; ++k)
-        if (wc_lds[k]) atomicAdd(S.stats + st_of[k], (unsigned long long)wc_lds[k]);
+    // the wave's counters into one of DT_STAT_SLOTS copies of the block (dt_collect_stats adds them
+    // up), one counter per lane: 5120 waves adding to the same words serialise on one L2 channel at
+    // the launch's end (the sky-item launch, a few hundred waves, keeps slot 0)
+    const int slot = DT_AGAIN_QUEUE && P.sky_again == 2 ? 0 : (int)(blockIdx.x % DT_STAT_SLOTS);
+    unsigned long long* const stb = slot == 0 ? S.stats : S.queue + DT_STAT_SLOT_OFF + (slot - 1) * DT_STAT_SLOT_STRIDE;
+    const int st_of[WC_N] = {ST_RAYS, ST_SHADOW, ST_TEX, ST_STACK, ST_REFL, ST_GLOSSY, ST_UV, ST_PRISM, ST_SPHL};
+    if (lane < WC_N) {
+      const unsigned long long v = wc_lds[lane];
+      if (v) atomicAdd(stb + st_of[lane], v);
+    } else if (lane == WC_N) {
+      if (cnt.wnodes) atomicAdd(stb + ST_WNODES, (unsigned long long)cnt.wnodes);
+    } else if (lane == WC_N + 1) {
+      if (sky_px) atomicAdd(stb + ST_SKY, sky_px);
     }
+
   }
 }
 

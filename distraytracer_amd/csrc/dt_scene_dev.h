@@ -216,6 +216,11 @@ struct DParams {
 #define DT_QSEG_MAX 8
 #define DT_QSEG_STRIDE 16
 #define DT_QSEG_OFF (1 + DT_N_STAMPS)   // from the queue word
+// copies 1..DT_STAT_SLOTS-1 of the ST_N counters (copy 0: the block's head), one per DT_STAT_SLOT_STRIDE
+// words from DT_STAT_SLOT_OFF past the queue word: wave b adds its counters to copy b % DT_STAT_SLOTS
+#define DT_STAT_SLOTS 16
+#define DT_STAT_SLOT_STRIDE 32
+#define DT_STAT_SLOT_OFF (DT_QSEG_OFF + DT_QSEG_MAX * DT_QSEG_STRIDE)
 
 // Tile ownership of the multi-GPU split: the tiles (raster order over the window) fall into groups
 // of `world` consecutive tiles, and slot s of rank r is tile s*world + (r + rot(s)) % world. Every

@@ -1,3 +1,4 @@
+# round-5 animate.py (one frame at a time), kept for the round-6 A/B of two frames in flight
 """C5 driver: render a range of animation frames of buildFinal(n*8) (scene.h:605-1100), each frame
 from fresh globals as the reference's one-process-per-frame runs do (Q23). Reports frames/s and
 Mpixel-samples/s, and per frame the conditions the reference aborts on, which must
@@ -32,7 +33,7 @@ import sys
 import time
 from concurrent.futures import ThreadPoolExecutor
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path.insert(0, ROOT)
 
 # the reference printf+throws / terminates on these (the device counts them), plus the
@@ -116,14 +117,7 @@ def main():
         n = next(mine, None)
         return ex.submit(prepare, n) if n is not None else None
 
-    # two frames in flight (frame-parallel modes): frame k renders on streams[k % 2] into imgs[k % 2];
-    # frame k+1's probe and render are enqueued before frame k is waited for, so its waves start on
-    # the CUs frame k's last items leave idle (each frame has its own scene object)
-    nbuf = 1 if args.split == "tiles" else 2
-    imgs = [torch.empty(3 * W * H if (args.split != "tiles" or rank == 0) else 1, dtype=torch.float32, device=dev)
-            for _ in range(nbuf)]
-    img = imgs[0]
-    streams = [torch.cuda.Stream(dev) for _ in range(nbuf)] if nbuf == 2 else None
+    img = torch.empty(3 * W * H if (args.split != "tiles" or rank == 0) else 1, dtype=torch.float32, device=dev)
     pipe = None
     if args.split == "tiles":
         g0 = dt.globals_default()
@@ -136,75 +130,40 @@ def main():
     g_res = dt.globals_default()
     g_res.xRes, g_res.yRes = W, H
     probe_tile = dt.tiles(rank=0, world=256, layout=dt.DT_OUT_SLAB)
-    probes = [torch.empty(max(dt.slab_floats(g_res, probe_tile), 1), dtype=torch.float32, device=dev)
-              for _ in range(nbuf)]
+    probe = torch.empty(max(dt.slab_floats(g_res, probe_tile), 1), dtype=torch.float32, device=dev)
     donated = 0
 
-    def choose_kernel(scene, g, n, k):
+    def choose_kernel(scene, g, n):
         """the trace kernel of frame n's scene (dt_scene_set_kernel, never the process environment:
         the worker thread is building the next scene meanwhile): the probe's rays per sample decide
-        (--donate auto). The probe renders on frame n's own stream."""
+        (--donate auto)"""
         if args.donate != "auto":
             scene.set_kernel(dt.DT_KERNEL_DONATE if args.donate == "on" else dt.DT_KERNEL_PRODUCT)
             return args.donate == "on", None
         scene.set_kernel(dt.DT_KERNEL_PRODUCT)
-        st_ = streams[k % 2].cuda_stream if streams else None
-        pst = dt.render(scene, g, n * 8, probes[k % nbuf], probe_tile, stream=st_)
+        pst = dt.render(scene, g, n * 8, probe, probe_tile)
         rps = pst.rays / max(pst.samples, 1)
         on = rps > args.donate_rps
         scene.set_kernel(dt.DT_KERNEL_DONATE if on else dt.DT_KERNEL_PRODUCT)
         return on, rps
-
-    def finish(job):
-        """wait for a frame rendered on its own stream, count it, write it, release its scene"""
-        nonlocal samples
-        n, g, scene, host_s, f1, k, dn_on, probe_rps = job
-        st = dt.collect_stats(scene, streams[k % 2].cuda_stream)   # (synchronizes that stream)
-        f2 = time.perf_counter()
-        samples += st.samples
-        for key in REPORTED:
-            aborts[key] += getattr(st, key)
-        done.append(n)
-        if args.per_frame:
-            rec = {"n": n, "frame": n * 8, "rank": rank, "host_ms": round(host_s * 1e3, 1),
-                   "render_ms": round((f2 - f1) * 1e3, 1), "spp": st.samples // max(st.pixels, 1),
-                   "donate": bool(dn_on), "probe_rays_per_sample": probe_rps and round(probe_rps, 3),
-                   "donations": st.donations, "donate_overflow": st.donate_overflow,
-                   "rays_per_sample": round(st.rays / max(st.samples, 1), 3), "sky_pixels": st.sky_pixels,
-                   "note": "render_ms: from its upload to its completion, with the previous frame in flight"}
-            rec.update({key: getattr(st, key) for key in REPORTED})
-            print(json.dumps(rec), file=sys.stderr, flush=True)
-        if args.out:
-            os.makedirs(args.out, exist_ok=True)
-            dt.write_png(os.path.join(args.out, "frame.%04d.png" % n), g, imgs[k % 2].cpu().numpy())
-        # released after the loop: hipFree waits for the whole device, which the next frame's render
-        # keeps busy, so a close here would serialise the frames again
-        finished.append(scene)
-
     # frame n+1's host build runs on a worker thread while frame n renders (ctypes releases the
     # GIL inside the library calls)
     with ThreadPoolExecutor(1) as ex:
         fut = next_job(ex)
         k = 0
-        inflight = None   # the previous frame, still rendering (frame-parallel modes)
-        finished = []
         while fut is not None:
             n, g, scene, host_s = fut.result()
             fut = next_job(ex)
             f1 = time.perf_counter()
             scene.upload()   # device half (a few ms), between renders
-            dn_on, probe_rps = choose_kernel(scene, g, n, k)
+            dn_on, probe_rps = choose_kernel(scene, g, n)
             donated += dn_on
             if pipe is None:
-                dt.render_async(scene, g, n * 8, imgs[k % 2], None, stream=streams[k % 2].cuda_stream)
-                if inflight is not None:
-                    finish(inflight)
-                inflight = (n, g, scene, host_s, f1, k, dn_on, probe_rps)
-                k += 1
-                continue
-            dt.render_async(scene, g, n * 8, pipe.slab(k), split.tile, stream=sh)
-            pipe.submit(k)   # gathers frame k, completes frame k-1 into the image
-            st = dt.collect_stats(scene, sh)
+                st = dt.render(scene, g, n * 8, img)
+            else:
+                dt.render_async(scene, g, n * 8, pipe.slab(k), split.tile, stream=sh)
+                pipe.submit(k)   # gathers frame k, completes frame k-1 into the image
+                st = dt.collect_stats(scene, sh)
             torch.cuda.synchronize()
             f2 = time.perf_counter()
             samples += st.samples
@@ -219,16 +178,13 @@ def main():
                        "rays_per_sample": round(st.rays / max(st.samples, 1), 3), "sky_pixels": st.sky_pixels}
                 rec.update({key: getattr(st, key) for key in REPORTED})
                 print(json.dumps(rec), file=sys.stderr, flush=True)
-            if args.out and rank == 0:
-                pipe.finish()
+            if args.out and (pipe is None or rank == 0):
+                if pipe is not None:
+                    pipe.finish()
                 os.makedirs(args.out, exist_ok=True)
                 dt.write_png(os.path.join(args.out, "frame.%04d.png" % n), g, img.cpu().numpy())
             scene.close()
             k += 1
-        if inflight is not None:
-            finish(inflight)
-        for sc in finished:
-            sc.close()
     if pipe is not None:
         pipe.finish()
     torch.cuda.synchronize()
