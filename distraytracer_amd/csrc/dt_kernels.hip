@@ -1883,8 +1883,8 @@ __device__ __noinline__ GeneralOcc<CNT> occluded_general(const DScene* S, const 
 }
 
 template <class CNT>
-__device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
-                                         V3 sstart, float t_max, int skip_shape, int li, float shift, CNT& cnt)
+__device__ __forceinline__ bool occluded_impl(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
+                                              V3 sstart, float t_max, int skip_shape, int li, float shift, CNT& cnt)
 {
   const Walk w = make_walk(P, active, sray, bstart, shift);
 #ifdef DT_STAMPS
@@ -2043,6 +2043,23 @@ static_assert(DT_SHAPE_TRIANGLE == 3, "DT_HAS(3) below");
 #endif
   if (w.bump_wave) return occluded_walk<2>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
   return occluded_walk<0>(S, P, w, active, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+}
+
+// the shadow test (occluded_impl); stamps builds: its cycles by path (69 cell list, 70 union of the
+// lanes' lists, 71 tree walks and the rest)
+template <class CNT>
+__device__ __forceinline__ bool occluded(const DScene& S, const DParams& P, bool active, V3 sray, V3 bstart, V3 sn,
+                                         V3 sstart, float t_max, int skip_shape, int li, float shift, CNT& cnt)
+{
+#ifdef DT_STAMPS
+  DT_T(oa);
+  const bool o = occluded_impl(S, P, active, sray, bstart, sn, sstart, t_max, skip_shape, li, shift, cnt);
+  DT_T(ob);
+  cnt.ph[69 + (cnt.cur_path == 0 ? 0 : cnt.cur_path == 1 ? 1 : 2)] += ob - oa;
+  return o;
+#else
+  return occluded_impl(S, P, active, sray, bstart, sn, sstart, t_max, skip_shape, li, shift, cnt);
+#endif
 }
 
 // =====================================================================================

@@ -57,6 +57,8 @@ def main():
           "tree-walk lanes %.2f, subtrees built for the light %.2f, a lane outside the grid %.2f, a block without a "
           "subtree %.2f, more blocks than DT_SG_SUB_MULTI %.2f"
           % (arr[63] / items, arr[64] / items, arr[65] / items, arr[66] / items, arr[67] / items, arr[68] / items))
+    print("shadow test cycles by path (%% of the kernel's): cell list %.2f%%, union %.2f%%, tree walks and other %.2f%%"
+          % (100.0 * arr[69] / max(tot, 1), 100.0 * arr[70] / max(tot, 1), 100.0 * arr[71] / max(tot, 1)))
     print("shadow walks per item: all occluded %.2f (%.1f visits/walk), none occluded %.2f (%.1f/walk), total %.2f"
           % (arr[29] / items, arr[28] / max(arr[29], 1), arr[31] / items, arr[30] / max(arr[31], 1), arr[9] / items))
     # per (light, shape) shadow tests: wave-level tests per item, lanes per test, lane hit fraction
