@@ -956,9 +956,12 @@ static int enqueue_render(dt_scene* sc, dtd::DParams P, const std::vector<float>
   PL.queue_segs = qs ? std::max(1, std::min(atoi(qs), DT_QSEG_MAX))
                      : (PL.world > 1 && (PL.chunks == 1 || PL.chunk_items) ? DT_QSEG_MAX : 1);
   // deep-cascade waves raise their priority (dt_kernels.hip, DT_PRIO_STEPS) when the frame is split
-  // over ranks, where one such wave bounds a rank's kernel; DT_PRIO_STEPS=<n> overrides (0: off)
+  // over ranks, where one such wave bounds a rank's kernel, and after 2 DFS steps in whole frames of
+  // several pixels per wave (spp < 64: C2, whose frame is bounded by a column of 30x-mean glossy items,
+  // profiles/r06h_tail_c2.log): C2 +0.9%, C3 +0.1%, C4 -0.4% (so not there; profiles/r06o_ab.txt).
+  // DT_PRIO_STEPS=<n> overrides (0: off)
   const char* ps = getenv("DT_PRIO_STEPS");
-  PL.prio_steps = ps ? atoi(ps) : (PL.world > 1 ? 8 : 0);
+  PL.prio_steps = ps ? atoi(ps) : (PL.world > 1 ? 8 : PL.ppw > 1 ? 2 : 0);
   // 1 spp (C5's cloud frames, n >= 244: nearly every pixel is sky): the trace kernel only flags
   // the missed pixels and dt_sky_miss_kernel marches their sky one pixel per lane, instead of the
   // wave marching each of its 64 pixels cooperatively in turn. DT_SKY_DEFER=0 disables it.
