@@ -1721,6 +1721,34 @@ __device__ __forceinline__ void shadow_leaf(const DScene& S, const DNodeDev& nd,
   DT_ACC(32, q0, q1);
 }
 
+#ifndef DT_SHAPE_FIRST
+#define DT_SHAPE_FIRST 1
+#endif
+// Shapes first (DT_SHAPE_FIRST, motion-blur passes): a leaf occludes a lane iff the reference gathers
+// it (bump_leaf_gathered) and the lane's segment hits one of its shapes. Both tests are exact, so
+// they may run in either order: the shapes first for the lanes whose bumped leaf box passes (the
+// gather's own first test), and the rest of the gather (the unbumped box, the parent chain) only for
+// the lanes with a hit. With large shifts the padded boxes pass for most segments and the shapes
+// miss (C5 frame 1920: no shadow hit in ~2900 lane tests per item), while the gather walks the
+// reference ancestors for every lane whose unbumped box fails.
+template <class CNT>
+__device__ __forceinline__ void shadow_leaf_bump(const DScene& S, const DNodeDev& nd, int r, const Walk& w,
+                                                 unsigned long long cand, unsigned long long& om, V3 bstart, V3 sn,
+                                                 V3 sstart, float t_max, int skip_shape, float shift, CNT& cnt)
+{
+  unsigned long long hit = 0;
+  shadow_leaf(S, nd, cand, hit, sn, sstart, t_max, skip_shape, shift, cnt);
+  if (hit) {
+    const bool g = bump_leaf_gathered(S, w, r, shift, bstart);
+    om |= __ballot(inv(hit) && g);
+  }
+}
+__device__ __forceinline__ bool bump_box(const DScene& S, const Walk& w, int r, float shift, V3 st)
+{
+  const DNodeDev rn = cas(S.nodes)[r];
+  return box_hit(rn, rn.lb[1] - shift, rn.ub[1] + shift, w.rb, st);
+}
+
 // an occluder at distance t' < t_max along sn from sstart sits at sray-parameter
 // u < 1 + 1e-3/|sray| from bstart; margins cover the f32 rounding
 __device__ __forceinline__ float shadow_tcull(float t_max)
@@ -1762,8 +1790,12 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
 #endif
     if (nd.meta & DN_LEAF) {
       DT_WK(DT_WK_BOX, BUMP && hb);
-      if (BUMP && hbm) hbm = __ballot(hb & bump_leaf_gathered(S, w, nd.skip, shift, bstart));
-      if (hbm) shadow_leaf(S, nd, hbm, om, sn, sstart, t_max, skip_shape, shift, cnt);
+      if (BUMP && DT_SHAPE_FIRST) {
+        if (hbm) shadow_leaf_bump(S, nd, nd.skip, w, hbm, om, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+      } else {
+        if (BUMP && hbm) hbm = __ballot(hb & bump_leaf_gathered(S, w, nd.skip, shift, bstart));
+        if (hbm) shadow_leaf(S, nd, hbm, om, sn, sstart, t_max, skip_shape, shift, cnt);
+      }
       if (GENERAL) {
         if (act) resume = inv(om) ? 0x7fffffff : nd.skip;
         if (!__ballot(resume != 0x7fffffff)) break;
@@ -1788,7 +1820,7 @@ __device__ __forceinline__ bool occluded_walk(const DScene& S, const DParams& P,
 // The shadow test over a cell's candidate list (host_shadowgrid.cpp): the same box test and
 // shape tests as the walk, on the only leaves that can hold an occluder for this cell and light.
 // BUMP: a motion-blur pass (lists built with sg_ypad >= bump_pad): the exact bumped gather test
-template <bool BUMP, class CNT>
+template <bool BUMP, class CNT, bool SF = false>
 __device__ bool occluded_list(const DScene& S, const Walk& w, bool active, V3 bstart, V3 sn, V3 sstart, float t_max,
                               int skip_shape, float shift, uint32_t off, uint32_t n, CNT& cnt)
 {
@@ -1799,12 +1831,17 @@ __device__ bool occluded_list(const DScene& S, const Walk& w, bool active, V3 bs
     const int r = uni(cas(S.sg_list)[off + k]);
     const DNodeDev nd = cas(S.nodes)[r];
     const bool live = inv(am & ~om);
-    const unsigned long long hbm = BUMP ? __ballot(live & bump_leaf_gathered(S, w, r, shift, bstart))
-                                        : (am & ~om) & box_mask_finite(nd, w.rb, bstart, tcull);
     DT_WK(DT_WK_BOX, live);
     DT_WK(DT_WK_BOX, BUMP && live);
     DT_CNT(34);
-    if (hbm) shadow_leaf(S, nd, hbm, om, sn, sstart, t_max, skip_shape, shift, cnt);
+    if (BUMP && SF) {
+      const unsigned long long cand = __ballot(live && bump_box(S, w, r, shift, bstart));
+      if (cand) shadow_leaf_bump(S, nd, r, w, cand, om, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+    } else {
+      const unsigned long long hbm = BUMP ? __ballot(live & bump_leaf_gathered(S, w, r, shift, bstart))
+                                          : (am & ~om) & box_mask_finite(nd, w.rb, bstart, tcull);
+      if (hbm) shadow_leaf(S, nd, hbm, om, sn, sstart, t_max, skip_shape, shift, cnt);
+    }
     if (!(am & ~om)) break;
   }
   return inv(om);
@@ -1832,7 +1869,7 @@ __device__ __forceinline__ int wave_min_u(int v)
 // lists are sorted by leaf index, built in leaf order), each leaf once, with the same exact box
 // test and shape tests as the walk. A lane testing a leaf outside its own list is harmless: the
 // box and shape tests are the reference's own, the list only bounds where an occluder can be.
-template <bool BUMP, class CNT>
+template <bool BUMP, class CNT, bool SF = false>
 __device__ bool occluded_union(const DScene& S, const Walk& w, bool active, V3 bstart, V3 sn, V3 sstart, float t_max,
                                int skip_shape, float shift, uint32_t off, uint32_t n, CNT& cnt)
 {
@@ -1848,12 +1885,17 @@ __device__ bool occluded_union(const DScene& S, const Walk& w, bool active, V3 b
     if (m == INT_MAX) break;
     const DNodeDev nd = cas(S.nodes)[m];
     const bool live = inv(am & ~om);
-    const unsigned long long hbm = BUMP ? __ballot(live & bump_leaf_gathered(S, w, m, shift, bstart))
-                                        : (am & ~om) & box_mask_finite(nd, w.rb, bstart, tcull);
     DT_WK(DT_WK_BOX, live);
     DT_WK(DT_WK_BOX, BUMP && live);
     DT_CNT(34);
-    if (hbm) shadow_leaf(S, nd, hbm, om, sn, sstart, t_max, skip_shape, shift, cnt);
+    if (BUMP && SF) {
+      const unsigned long long cand = __ballot(live && bump_box(S, w, m, shift, bstart));
+      if (cand) shadow_leaf_bump(S, nd, m, w, cand, om, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
+    } else {
+      const unsigned long long hbm = BUMP ? __ballot(live & bump_leaf_gathered(S, w, m, shift, bstart))
+                                          : (am & ~om) & box_mask_finite(nd, w.rb, bstart, tcull);
+      if (hbm) shadow_leaf(S, nd, hbm, om, sn, sstart, t_max, skip_shape, shift, cnt);
+    }
     if (head == m) {
       ++k;
       head = nxt;
@@ -1941,8 +1983,9 @@ __device__ __forceinline__ bool occluded_impl(const DScene& S, const DParams& P,
 #ifdef DT_STAMPS
         cnt.cur_path = 0;
 #endif
-        return bump_list ? occluded_list<true>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, off, n, cnt)
-                         : occluded_list<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, off, n, cnt);
+        if (bump_list)
+          return occluded_list<true, CNT, DT_SHAPE_FIRST>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, off, n, cnt);
+        return occluded_list<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, off, n, cnt);
       }
       DT_CNT(37);
     }
@@ -1974,8 +2017,9 @@ __device__ __forceinline__ bool occluded_impl(const DScene& S, const DParams& P,
 #ifdef DT_STAMPS
         cnt.cur_path = 1;
 #endif
-        return bump_list ? occluded_union<true>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt)
-                         : occluded_union<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
+        if (bump_list)
+          return occluded_union<true, CNT, DT_SHAPE_FIRST>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt);
+        return occluded_union<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
       }
 // (bit 3: DT_SHAPE_TRIANGLE is an enum constant, which #if would read as 0; rounds 4-5 had that, so
 // this block was compiled out of the mesh builds)
@@ -3418,13 +3462,15 @@ DT_TRACE_KERNEL(const DLaunch* __restrict__ Lp, float* __restrict__ out)
     const int slot = DT_AGAIN_QUEUE && P.sky_again == 2 ? 0 : (int)(blockIdx.x % DT_STAT_SLOTS);
     unsigned long long* const stb = slot == 0 ? S.stats : S.queue + DT_STAT_SLOT_OFF + (slot - 1) * DT_STAT_SLOT_STRIDE;
     const int st_of[WC_N] = {ST_RAYS, ST_SHADOW, ST_TEX, ST_STACK, ST_REFL, ST_GLOSSY, ST_UV, ST_PRISM, ST_SPHL};
+    const unsigned long long sky_w = __shfl(sky_px, 0);   // (lane 0's, as before: counted there)
+    const unsigned int wn_w = __shfl((unsigned int)cnt.wnodes, 0);
     if (lane < WC_N) {
       const unsigned long long v = wc_lds[lane];
       if (v) atomicAdd(stb + st_of[lane], v);
     } else if (lane == WC_N) {
-      if (cnt.wnodes) atomicAdd(stb + ST_WNODES, (unsigned long long)cnt.wnodes);
+      if (wn_w) atomicAdd(stb + ST_WNODES, (unsigned long long)wn_w);
     } else if (lane == WC_N + 1) {
-      if (sky_px) atomicAdd(stb + ST_SKY, sky_px);
+      if (sky_w) atomicAdd(stb + ST_SKY, sky_w);
     }
 
   }
