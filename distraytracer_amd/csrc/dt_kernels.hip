@@ -1455,6 +1455,18 @@ __device__ __forceinline__ bool bump_leaf_gathered(const DScene& S, const Walk& 
   return ok;
 }
 
+// Closest hit with shapes first (closest_hit_walk, closest_hit_plist: blur passes) needs shape tests
+// that read no earlier test's state: not with checkerboards (the edge-on case reuses the previous t,
+// Q16), so only in the builds without them (the tunnel builds: C5's frames with motion blur)
+#ifndef DT_SHAPE_FIRST
+#define DT_SHAPE_FIRST 1
+#endif
+static_assert(DT_SHAPE_CHECKERBOARD == 6 && DT_SHAPE_CHECKERBOARD_HOLE == 7 && DT_SHAPE_CHECKER_CYLINDER == 8,
+              "DT_HAS(6/7/8) below");
+#ifndef DT_SF_CLOSEST
+#define DT_SF_CLOSEST (DT_SHAPE_FIRST && !DT_HAS(6) && !DT_HAS(7) && !DT_HAS(8))
+#endif
+
 // every active lane's motion-blur shift lies within the bump tree's padding, and is >= 0 when the
 // tree (and the blur-padded grid lists) were padded for non-negative shifts only (host_accel.cpp):
 // the render's globals may draw shifts the build's did not
@@ -1501,7 +1513,48 @@ __device__ __forceinline__ bool closest_hit_walk(const DScene& S, const DParams&
     DT_CNT(26);
     if (nd.meta & DN_LEAF) {
       DT_WK(DT_WK_BOX, BUMP && hb);   // the exact bumped gather: the reference leaf's own box test
-      if (BUMP && hbm) hbm = __ballot(hb & bump_leaf_gathered(S, w, nd.skip, shift, org));
+      if (BUMP && DT_SF_CLOSEST) {
+        // shapes first into a tentative record, the exact gather only for the lanes with a hit
+        // (shadow_leaf_bump): the same result in either order, as no shape test here reads an
+        // earlier test's state (no checkerboards in these builds: DT_SF_CLOSEST)
+        if (hbm) {
+          HitRec th = h;
+          bool tany = false, chg = false;
+          const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
+          for (int q = 0; q < nq; ++q) {
+            int sid, type, off;
+            uint32_t flags;
+            leaf_shape(S, nd, q, sid, type, flags, off);
+            DT_CNT(8);
+            DT_CNT(10 + (type & 7));
+            if (inv(hbm)) {
+              DT_WK(DT_WK_HIT_SHAPE + type, true);
+              int ins = 0, cc = -1;
+              if (shape_hit(S, sid, type, flags, cas(S.geom) + off, ray, org, shift, t_dist, ins, cc, th.edge)) {
+                tany = true;
+                const int rank = ftree ? (int)(nd.meta >> 16) : 0;
+                if (t_dist < th.t_min || (ftree && t_dist == th.t_min && rank < th.rank)) {
+                  th.rank = rank;
+                  th.shape = sid;
+                  th.inside = ins;
+                  th.t_min = t_dist;
+                  th.ccol = cc;
+                  chg = true;
+                }
+              }
+            }
+          }
+          if (__ballot(tany)) {
+            const bool g = bump_leaf_gathered(S, w, nd.skip, shift, org);
+            if (tany && g) {
+              any = true;
+              if (chg) h = th;
+            }
+          }
+        }
+        hbm = 0;
+      }
+      if (BUMP && !DT_SF_CLOSEST && hbm) hbm = __ballot(hb & bump_leaf_gathered(S, w, nd.skip, shift, org));
       if (hbm) {
         DT_T(q0);
         const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
@@ -1570,9 +1623,47 @@ __device__ __forceinline__ bool closest_hit_plist(const DScene& S, const DParams
     unsigned long long hbm = am & box_mask_finite(nd, w.rb, org, tcull);
     DT_WK(DT_WK_BOX, active);
     DT_WK(DT_WK_BOX, BUMP && inv(hbm));
-    if (BUMP && hbm) hbm = __ballot(inv(hbm) & bump_leaf_gathered(S, w, nd.skip, shift, org));
     DT_WORK(cnt.wnodes++);
     DT_CNT(26);
+    if (BUMP && DT_SF_CLOSEST) {   // shapes first, then the exact gather (closest_hit_walk)
+      if (hbm) {
+        HitRec th = h;
+        bool tany = false, chg = false;
+        const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
+        const int rank = (int)(nd.meta >> 16);
+        for (int q = 0; q < nq; ++q) {
+          int sid, type, off2;
+          uint32_t flags;
+          leaf_shape(S, nd, q, sid, type, flags, off2);
+          DT_CNT(8);
+          DT_CNT(10 + (type & 7));
+          if (inv(hbm)) {
+            DT_WK(DT_WK_HIT_SHAPE + type, true);
+            int ins = 0, cc = -1;
+            if (shape_hit(S, sid, type, flags, cas(S.geom) + off2, ray, org, shift, t_dist, ins, cc, th.edge)) {
+              tany = true;
+              if (t_dist < th.t_min || (t_dist == th.t_min && rank < th.rank)) {
+                th.rank = rank;
+                th.shape = sid;
+                th.inside = ins;
+                th.t_min = t_dist;
+                th.ccol = cc;
+                chg = true;
+              }
+            }
+          }
+        }
+        if (__ballot(tany)) {
+          const bool g = bump_leaf_gathered(S, w, nd.skip, shift, org);
+          if (tany && g) {
+            any = true;
+            if (chg) h = th;
+          }
+        }
+      }
+      hbm = 0;
+    }
+    if (BUMP && !DT_SF_CLOSEST && hbm) hbm = __ballot(inv(hbm) & bump_leaf_gathered(S, w, nd.skip, shift, org));
     if (hbm) {
       const int nq = (nd.meta & DN_SINGLE) ? 1 : nd.aux;
       const int rank = (int)(nd.meta >> 16);
