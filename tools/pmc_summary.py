@@ -56,7 +56,11 @@ def main(tag, kernel="dt_trace_kernel", config="c3"):
         json.dump(out, fh, indent=1, sort_keys=True)
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(ROOT, "profiles", "%s_kernel_stats.csv" % tag))
-    # the profile bench.py's roofline.traffic reads (the latest summarised tag)
+    # the profile bench.py's roofline.traffic reads (the latest summarised tag of the bench's default
+    # config, C3: a profile of another config would leave the default bench line without one)
+    if config != "c3":
+        print(json.dumps(out, indent=1, sort_keys=True))
+        return out
     with open(os.path.join(ROOT, "profiles", "pmc_trace_summary.json"), "w") as fh:
         d = {k: out.get(k) for k in ("tag", "kernel", "avg_duration_ns", "hbm_bytes_per_launch",
                                      "valu_active_per_wave_cycle", "valu_lane_utilisation", "waves_per_simd",
