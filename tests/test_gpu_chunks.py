@@ -1,6 +1,7 @@
 """Chunk items (spp > 64): every 64-sample chunk of a pixel is a queue item of its own, so a pixel's
-chunks run on different waves, and the chunk that completes the pixel adds all of its sample colours
-in sample order (dt_kernels.hip item loop, dt_api.cpp enqueue_render). The reference sums a pixel's
+chunks run on different waves; each chunk stores its sample colours, and dt_chunk_sum_kernel, launched
+after the trace (and sky-item) launches, adds each pixel's colours in sample order (dt_kernels.hip item
+loop and dt_chunk_sum_kernel, dt_api.cpp enqueue_render). The reference sums a pixel's
 samples in order (render_final_project.cpp:1062-1213: `color += tmp_color` per sample, then
 `/= sampled_n`), so the images must be bit-identical to the per-pixel items (DT_CHUNK_ITEMS=0, one
 wave running the chunks in turn) and to the oracle, for:
@@ -10,9 +11,9 @@ wave running the chunks in turn) and to the oracle, for:
     on different waves and, at any grid, in different phases of the launch);
   * spp that leave a partial last chunk (81, 100, 144 spp: 17, 36, 16 samples);
   * the sky-item launch (still builds list a chunk with a missed sample; the *_sky build renders the
-    listed chunks again and the last of them completes the pixel): the spheres scene with clouds;
-  * a motion-blur build (tunnel frame), and renders repeated on one scene (the arrival words are
-    zeroed by the wave that completes a pixel, so the next launch starts clean).
+    listed chunks again, storing their colours over the first launch's): the spheres scene with clouds;
+  * a motion-blur build (tunnel frame), and renders repeated on one scene (the colour buffer is
+    reused from launch to launch; every chunk overwrites its own slots, so nothing carries over).
 """
 import numpy as np
 import pytest
@@ -80,9 +81,8 @@ def test_c4_chunk_items(cuda, monkeypatch):
 
 @pytest.mark.parametrize("aa,depth", [(81, 4), (100, 3), (144, 2)])
 def test_partial_last_chunk(cuda, monkeypatch, aa, depth):
-    """spp = 81, 100, 144: the last chunk holds 17, 36, 16 samples. The C4 scene (mesh build: chunk
-    items) and the C3 scene (room build, which carries no chunk code: the host keeps per-pixel items
-    whatever DT_CHUNK_ITEMS says, and this checks that choice)."""
+    """spp = 81, 100, 144: the last chunk holds 17, 36, 16 samples. The C4 scene (mesh build) and the C3
+    scene (room build); both builds carry the chunk code."""
     for models in (0, 1):
         g = dt.globals_default()
         g.use_model = models
@@ -96,8 +96,8 @@ def test_partial_last_chunk(cuda, monkeypatch, aa, depth):
 def test_chunk_items_sky_launch(cuda, monkeypatch, aa, world):
     """The spheres scene with perlin_cloud (sky around the spheres) at spp > 64: the still build
     lists every chunk with a missed sample, the *_sky build renders those chunks again, and the
-    last listed chunk to arrive completes the pixel. Whole image and a slab split, each mode
-    rendered twice on one scene (arrival words reset between launches)."""
+    sum kernel adds the colours after both launches. Whole image and a slab split, each mode
+    rendered twice on one scene."""
     g = dt.globals_default()
     built = dt.build_scene("spheres", 0, g)
     g.perlin_cloud = 1
