@@ -4,8 +4,9 @@ Every rank holds the whole (tiny) scene and renders one tile of every group of `
 consecutive tiles (raster order), the ranks rotated by a hash of the group (dt_scene_dev.h
 tile_of), into a packed slab: the expensive sky/glossy regions spread over all GPUs, and unlike a
 plain t % world interleave no rank is tied to a fixed set of tile columns. The tile side follows
-the world size (tile_side): 8x8 (the primary lists' block) at every N > 1, where many tiles per
-rank even out the ranks' work, and 2x2 for pixels of several 64-sample chunks (spp > 64, C4). Rank-balance kernel times of C3 (profiles/r04zs_rank_balance_tiles.log,
+the world size and the samples per pixel (tile_side): 2x2 for pixels of several 64-sample chunks
+(spp > 64, C4) at every N > 1 and for one-wave pixels (C3) from N = 4 on, 8x8 (the primary lists'
+block) otherwise; many tiles per rank even out the ranks' work. Rank-balance kernel times of C3 (profiles/r04zs_rank_balance_tiles.log,
 slowest share 8x8 against 16x16): N=2 17.60 against 17.75 ms, N=4 9.09 against 9.12, N=8 4.73
 against 4.87 (round 3: slowest rank 6.29 -> 5.96 ms from 32x32, profiles/r03z_rank_balance_tiles.log).
 32x32 at N = 1, where the waves that run at once cover a compact part of the image: at world 1 the
@@ -27,12 +28,20 @@ def tile_side(world, spp=64):
     0.985 / 0.978 / 0.930 with 4x4, 0.986 / 0.956 / 0.915 with 8x8 and 0.974 / 0.980 / 0.871 with
     16x16 (profiles/r06g_rb_t4.log, r06g_rb_t8.log, r06g_rb_t16.log). The cost is concentrated: the
     longest 1% of C4's chunk items hold ~47% of the wave time, in a few clusters of mesh pixels
-    (profiles/r06e_costs_c4_w8.log), and small tiles spread each cluster over every rank."""
+    (profiles/r06e_costs_c4_w8.log), and small tiles spread each cluster over every rank.
+    Pixels of one wave each (33..64 samples: C3) take 2x2 from N = 4 on and 8x8 at N = 2 (two runs
+    of each, C3, two frames in flight, profiles/r06s_rb_c3_t8a/b.log, r06s_rb_c3_t2a/b.log): the
+    slowest share at N = 8 4.431 / 4.417 ms with 2x2 against 4.440 / 4.457 with 8x8, at N = 4
+    8.632 / 8.597 against 8.632 / 8.624, at N = 2 16.988 / 17.003 against 16.915 / 16.944. Several
+    pixels per wave (spp <= 32: C2) keep 8x8 (profiles/r06i_rb_c2_t4.log, r06i_rb_c2_t8.log)."""
     if world <= 1:
         return 32
     # the samples the kernel takes: int(sqrt(aa))^2 (host_flatten.cpp; aa = 65..80 is one chunk)
     import math
-    return 2 if int(math.isqrt(max(int(spp), 1))) ** 2 > 64 else 8
+    s = int(math.isqrt(max(int(spp), 1))) ** 2
+    if s > 64:
+        return 2
+    return 2 if s > 32 and world >= 4 else 8
 
 
 class FrameSplit:

@@ -30,6 +30,9 @@ def _scene(cfg):
     if cfg == "final":
         b = dt.build_scene("final", 240, g)
         g.xRes, g.yRes, g.antialias_samples, g.max_depth = 72, 40, 4, 3
+    elif cfg == "final64":   # one pixel per wave: 2x2 split tiles from world 4 on (tile_side)
+        b = dt.build_scene("final", 240, g)
+        g.xRes, g.yRes, g.antialias_samples, g.max_depth = 38, 22, 64, 2
     else:
         b = dt.build_scene("spheres", 0, g)
         g.xRes, g.yRes, g.antialias_samples, g.max_depth = 70, 45, 1, 1
@@ -101,7 +104,7 @@ def test_gather_pipeline_double_buffer(tmp_path):
         assert np.array_equal(got[k], ref), k
 
 
-@pytest.mark.parametrize("world,cfg", [(2, "final"), (3, "spheres")])
+@pytest.mark.parametrize("world,cfg", [(2, "final"), (3, "spheres"), (4, "final64")])
 def test_tile_split_gather_equals_single_rank(tmp_path, world, cfg):
     import distraytracer_amd as dt
     import oracle
@@ -192,3 +195,16 @@ def test_frame_queue_single_process():
     from distraytracer_amd.multigpu import FrameQueue
     q = FrameQueue([5, 1, 3, 9], {5: 1.0, 1: 10.0, 9: 10.0})   # 3 unknown: the mean (7)
     assert list(q) == [1, 9, 3, 5]
+
+
+def test_tile_side_rule():
+    """multigpu.tile_side: 32 for a whole frame, 2x2 for multi-chunk pixels at N > 1 (keyed on the
+    samples the kernel takes, int(sqrt(aa))^2: aa = 80 is one chunk), 2x2 for one-wave pixels from
+    N = 4 on, 8x8 for several pixels per wave (profiles/r06s_*, r06i_*, r06h_*)."""
+    from distraytracer_amd.multigpu import tile_side
+    assert tile_side(1, 64) == 32 and tile_side(1, 256) == 32
+    assert [tile_side(n, 256) for n in (2, 4, 8)] == [2, 2, 2]
+    assert [tile_side(n, 64) for n in (2, 4, 8)] == [8, 2, 2]
+    assert [tile_side(n, 80) for n in (2, 8)] == [8, 2]      # 64 samples taken: one chunk
+    assert [tile_side(n, 81) for n in (2, 8)] == [2, 2]      # 81: two chunks
+    assert [tile_side(n, 16) for n in (2, 4, 8)] == [8, 8, 8]
