@@ -642,6 +642,13 @@ static int prepare_render(const dt_scene* sc, const dt_globals* g, int32_t frame
   const char* smu = getenv("DT_SG_SUB_MULTI");
   P.sgb_multi = smu && atoi(smu) > 0 ? atoi(smu) : 1;
   P.sg_ypad = (float)sc->sg.ypad;
+  // start-side culling (host_shadowgrid.cpp) assumed every ray origin inside sg.org_lo..org_hi: a
+  // camera whose eye region (eye +- the aperture) leaves it walks the trees instead of the lists
+  if (sc->sg.org_check) {
+    const double r = std::fabs((double)P.aperture);
+    for (int a = 0; a < 3; ++a)
+      if (!(P.eye[a] - r >= sc->sg.org_lo[a] && P.eye[a] + r <= sc->sg.org_hi[a])) P.sg_n = 0;
+  }
 
   P.n_lights = (int32_t)sc->flat.lights.size();
   P.ls_first = 0;

@@ -117,7 +117,7 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
   const char* sgr = getenv("DT_SG_REACH");
   if ((sgv && sgv[0] == '0') || a.no_cull ||
       !build_shadow_grid(dnodes, f, a.sg, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : DT_SG_REACH_DEFAULT,
-                         a.n_bnodes > 0 ? (double)a.bump_pad : 0.0, up_only))
+                         a.n_bnodes > 0 ? (double)a.bump_pad : 0.0, up_only, g.eye, (double)g.aperture))
     a.sg = ShadowGrid();
   for (int l = 0; l < DT_MAX_SGRID; ++l) a.sg.base0[l] = a.sg.base[l];
   // Large blur shifts pad the lists until most cells overflow and walk the tree, pass-0 rays
@@ -153,9 +153,9 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
       mx = std::max(mx, (size_t)n);
     }
     fprintf(stderr, "shadow grid: lights %d dim %dx%dx%d cells %zu (tree %zu) mean list %.2f max %zu list pool %zu "
-            "plane-culled %ld umbra cells %ld ypad %g hash %016llx\n",
+            "plane-culled %ld (start-side %ld) umbra cells %ld ypad %g hash %016llx\n",
             a.sg.n_lights, a.sg.dim[0], a.sg.dim[1], a.sg.dim[2], cells, tree,
-            cells > tree ? (double)sum / (cells - tree) : 0.0, mx, a.sg.list.size(), a.sg.plane_dropped, a.sg.umbra_cells, a.sg.ypad,
+            cells > tree ? (double)sum / (cells - tree) : 0.0, mx, a.sg.list.size(), a.sg.plane_dropped, a.sg.start_dropped, a.sg.umbra_cells, a.sg.ypad,
             (unsigned long long)sg_hash(a.sg, false));
   }
   stage("shadow grid");

@@ -57,6 +57,12 @@ struct ShadowGrid {
   std::vector<uint32_t> sub_blocks;      // (first node, node count) per block; count 0: none
   std::vector<dtd::DNodeDev> sub_nodes;
   long plane_dropped = 0;            // (leaf, cell) pairs left out by plane culling (diagnostic)
+  long start_dropped = 0;            // of those, by start-side culling (diagnostic)
+  // start-side culling assumed every ray origin inside this box (the root box and the camera's
+  // eye region at build time); a render whose camera leaves it must not use the lists
+  // (dt_api.cpp prepare_render)
+  bool org_check = false;
+  double org_lo[3] = {0, 0, 0}, org_hi[3] = {0, 0, 0};
   long umbra_cells = 0;              // (light, cell) records flagged DT_SG_UMBRA (diagnostic)
 };
 struct FlatScene;
@@ -96,8 +102,11 @@ inline void blur_leaf_pad(const dtd::DNodeDev& n, double ypad, bool up_only, dou
     above = (flags & DT_F_NAMED_RECT) ? ypad : 0;
   }
 }
+// cam / cam_r: the camera's eye and aperture radius (start-side culling, host_shadowgrid.cpp header;
+// null: off)
 bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene& fs, ShadowGrid& g,
-                       double target_cells = 32768, float reach = 0.5f, double ypad = 0, bool up_only = false);
+                       double target_cells = 32768, float reach = 0.5f, double ypad = 0, bool up_only = false,
+                       const double* cam = nullptr, double cam_r = 0);
 
 // device-layout scene produced from a descriptor (host_flatten.cpp)
 struct FlatScene {

@@ -47,6 +47,40 @@
 // far enough from the start for the reference's leaf-box test from isectP + 1e-3 sray to pass,
 // so the reference's gather holds the face's leaf: its shadow test answers "occluded" as well.
 //
+// Start-side culling: a cell next to a wall contains points of the wall
+// itself, so the wall's plane meets the cell box and plane culling keeps it, though no shadow
+// segment from a point on the wall (or in front of it) to a light in front of it can cross it. The
+// reference's test (rect_plane_hit, geometry.cpp:640-741) starts at o = p + 1e-3 sn and reports a
+// hit only at t_final = (float)(((A - o).n) / (float)(sn.n)) in (eps, t_max). Write d(x) = s (n.x - c)
+// for the plane (unit n), s the side of the light box, D = min d over the light box (> 0). Then
+// d(o) = (1 - l) d(p) + l d(q) with l = 1e-3 / |q - p| <= 1e-3 / Lmax, so d(o) >= min(d(p), 0) +
+// 1e-3 D / Lmax; the segment's end q + 1e-3 sn has d >= D - 1e-3; d is linear along the ray, so
+// when both ends are positive the ray never reaches the plane in [0, t_max]: the numerator's sign
+// (double, exact far below the margins) makes t_final negative when the ray moves away from the
+// plane, and beyond t_max by the relative gap d(end) / d(o) >= (D - 1e-3) / maxdist when it moves
+// toward it (the float roundings of t_final and t_max are ~1e-7 relative). What remains is a lower
+// bound of d(p) over the shading points p that use the cell's list: the points of the widened
+// cell box that some closest-hit test reported. Such a p = start + t_f ray has an exact
+// counterpart X* = start + t* ray on (or, for a near miss of the float tests, within rho of) the
+// shape's box, with |t_f - t*| <= eta |t*|: eta 1e-6 for the plane tests (rectangles,
+// checkerboards, prism faces: a float ratio of a double numerator, ~1.2e-7), 4e-3 for the float
+// quadratics of spheres and cylinders near tangency (sqrt(2^-24) ~ 2.4e-4) and for triangles. So
+// |d(p) - d(X*)| <= eta |d(X*) - d(start)| <= 2 eta maxdist, where maxdist bounds |d| over every
+// ray origin (the root box and the camera's eye region, 2% more for the origins of secondary rays
+// off the hit points), and p lies within eta times the origin box's diagonal of X*, and within 1e-3 of the start o from
+// which the device picks the cell (pad: the sum, + 1e-3). Per cell
+// and class (plane tests / quadratics) the host keeps the bounding box of {shape box + rho} ^ {cell
+// box + pad} over the shapes that meet it; d's minimum over those boxes, less 2 eta maxdist, is
+// the bound. A wall is then left out of a cell's list for a light when that bound, plus
+// 1e-3 D / Lmax, stays above 1e-7 (1 + scale), D - 1e-3 above 1e-5 maxdist, and the cell box
+// keeps 2e-3 from the light box. The origin box is recorded: a render whose camera's eye region
+// leaves it walks the trees (dt_api.cpp prepare_render). Only axis-aligned planes profit (a tilted
+// shape's box is not flat), and only rectangles and checkerboards are tried as the culled shape.
+// With ypad > 0 (blur passes) every "rectangle" moves by up to ypad in y: its box grows by ypad in
+// y, and as the culled shape its plane moves by |n_y| ypad (nothing for a wall with a horizontal
+// normal), which D and the bound lose. C3: the back and side walls leave the lists of the boundary cells for the four
+// ceiling lights.
+//
 // Motion blur: with ypad > 0 the lists also serve the blur passes (bumped leaf boxes, "rectangle"
 // shapes shifted by |val| <= ypad in y): leaf boxes are padded by ypad in y, and a moving
 // rectangle's plane must clear the hull by ypad more.
@@ -210,7 +244,7 @@ bool shape_separated(const dtd::DShapeHdr& h, const double* g, const double clo[
 }  // namespace
 
 bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene& fs, ShadowGrid& g,
-                       double target_cells, float reach, double ypad, bool up_only)
+                       double target_cells, float reach, double ypad, bool up_only, const double* cam, double cam_r)
 {
   const double t_entry = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
   const std::vector<dtd::DLight>& lights = fs.lights;
@@ -301,7 +335,165 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       for (int64_t q = 0; q < (int64_t)nd.aux; ++q) out.push_back(fs.bvh.leaf_idx[nd.first + q]);
   };
   long dropped = 0;
+  std::atomic<long> start_dropped(0);
   const bool timing = getenv("DT_TIMING") != nullptr;
+  // start-side culling (header); DT_SG_START=0 disables it
+  const char* sg_start_env = getenv("DT_SG_START");
+  const bool start_on = cam != nullptr && !(sg_start_env && sg_start_env[0] == '0');
+  const size_t nshape = fs.hdr.size();
+  const int ncell_all = g.dim[0] * g.dim[1] * g.dim[2];
+  const double eta_k[2] = {1e-6, 4e-3};   // plane tests; quadratics and triangles
+  std::vector<double> occ;                 // per cell and class: box (lo[3], hi[3]) of possible shading points
+  std::vector<int8_t> s_plane;             // shapes tried as the culled one: 1 (unit normal in s_n, offset s_c)
+  std::vector<double> s_n, s_c, s_maxd, s_move;
+  if (start_on) {
+    double olo[3], ohi[3];
+    for (int a = 0; a < 3; ++a) {
+      olo[a] = std::min((double)nodes[0].lb[a], cam[a] - cam_r);
+      ohi[a] = std::max((double)nodes[0].ub[a], cam[a] + cam_r);
+    }
+    g.org_check = true;
+    for (int a = 0; a < 3; ++a) { g.org_lo[a] = olo[a]; g.org_hi[a] = ohi[a]; }
+    double diag = 0;
+    for (int a = 0; a < 3; ++a) diag += (ohi[a] - olo[a]) * (ohi[a] - olo[a]);
+    diag = std::sqrt(diag) * 1.02;
+    occ.assign((size_t)ncell_all * 12, 0.0);
+    for (size_t c = 0; c < (size_t)ncell_all * 2; ++c)
+      for (int a = 0; a < 3; ++a) { occ[c * 6 + a] = INFINITY; occ[c * 6 + 3 + a] = -INFINITY; }
+    std::vector<P3> pts;
+    for (size_t sid = 0; sid < nshape; ++sid) {
+      const dtd::DShapeHdr& hd = fs.hdr[sid];
+      const double* gp = fs.geom.data() + hd.off;
+      double blo[3], bhi[3];
+      int k = 1;
+      pts.clear();
+      if (hd.type == DT_SHAPE_SPHERE) {
+        const double r = std::sqrt(gp[dtd::SP_R2]);
+        for (int a = 0; a < 3; ++a) { blo[a] = gp[dtd::SP_C + a] - r; bhi[a] = gp[dtd::SP_C + a] + r; }
+      } else if (hd.type == DT_SHAPE_CYLINDER || hd.type == DT_SHAPE_CHECKER_CYLINDER) {
+        const double r = std::sqrt(gp[dtd::CY_R2]);
+        for (int a = 0; a < 3; ++a) {
+          blo[a] = std::min(gp[dtd::CY_C1 + a], gp[dtd::CY_C2 + a]) - r;
+          bhi[a] = std::max(gp[dtd::CY_C1 + a], gp[dtd::CY_C2 + a]) + r;
+        }
+      } else if (shape_hull_points(hd, gp, 0.0, pts) && !pts.empty()) {
+        k = (hd.type == DT_SHAPE_TRIANGLE) ? 1 : 0;
+        for (int a = 0; a < 3; ++a) { blo[a] = INFINITY; bhi[a] = -INFINITY; }
+        for (const P3& q : pts)
+          for (int a = 0; a < 3; ++a) { blo[a] = std::min(blo[a], q[a]); bhi[a] = std::max(bhi[a], q[a]); }
+      } else {   // a shape type without bounds here: nothing is start-culled
+        occ.clear();
+        break;
+      }
+      if (ypad > 0 && hd.type == DT_SHAPE_RECTANGLE && (hd.flags & DT_F_NAMED_RECT)) {   // moves in the blur passes
+        blo[1] -= ypad;
+        bhi[1] += ypad;
+      }
+      double sd = 0;
+      for (int a = 0; a < 3; ++a) sd += (bhi[a] - blo[a]) * (bhi[a] - blo[a]);
+      const double rho = 1e-6 * (1 + std::sqrt(sd));
+      // + 2e-3: the device picks the cell from o = p + 1e-3 sn, not from p
+      const double pad = eta_k[k] * diag + 2e-3;
+      for (int a = 0; a < 3; ++a) { blo[a] -= rho; bhi[a] += rho; }
+      int i0[3], i1[3];
+      bool any = true;
+      for (int a = 0; a < 3; ++a) {
+        // cells whose widened box [lo + i h - m1, lo + (i + 1) h + m1] meets [blo - pad, bhi + pad]
+        i0[a] = std::max(0, (int)std::ceil((blo[a] - pad - m1 - lo[a]) / hh[a] - 1) - 1);
+        i1[a] = std::min(g.dim[a] - 1, (int)std::floor((bhi[a] + pad + m1 - lo[a]) / hh[a]) + 1);
+        if (i0[a] > i1[a]) any = false;
+      }
+      if (!any) continue;
+      for (int z = i0[2]; z <= i1[2]; ++z)
+        for (int y = i0[1]; y <= i1[1]; ++y)
+          for (int x = i0[0]; x <= i1[0]; ++x) {
+            const int ci[3] = {x, y, z};
+            double clo[3], chi[3];
+            bool meet = true;
+            for (int a = 0; a < 3; ++a) {
+              clo[a] = std::max(blo[a], lo[a] + ci[a] * hh[a] - m1 - pad);
+              chi[a] = std::min(bhi[a], lo[a] + (ci[a] + 1) * hh[a] + m1 + pad);
+              if (clo[a] > chi[a]) meet = false;
+            }
+            if (!meet) continue;
+            double* o = occ.data() + (((size_t)z * g.dim[1] + y) * g.dim[0] + x) * 12 + k * 6;
+            for (int a = 0; a < 3; ++a) { o[a] = std::min(o[a], clo[a]); o[3 + a] = std::max(o[3 + a], chi[a]); }
+          }
+    }
+    if (!occ.empty()) {
+      s_plane.assign(nshape, 0);
+      s_n.assign(nshape * 3, 0.0);
+      s_c.assign(nshape, 0.0);
+      s_maxd.assign(nshape, 0.0);
+      s_move.assign(nshape, 0.0);
+      for (size_t sid = 0; sid < nshape; ++sid) {
+        const dtd::DShapeHdr& hd = fs.hdr[sid];
+        const double* R = nullptr;
+        if (hd.type == DT_SHAPE_RECTANGLE) R = fs.geom.data() + hd.off + dtd::RC_R;
+        else if (hd.type == DT_SHAPE_CHECKERBOARD || hd.type == DT_SHAPE_CHECKERBOARD_HOLE) R = fs.geom.data() + hd.off + dtd::CK_R;
+        if (!R) continue;
+        const double* n = R + dtd::R_N;
+        const double nn = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        if (!(nn > 0) || !std::isfinite(nn)) continue;
+        for (int a = 0; a < 3; ++a) s_n[sid * 3 + a] = n[a] / nn;
+        s_c[sid] = s_n[sid * 3] * R[dtd::R_A] + s_n[sid * 3 + 1] * R[dtd::R_A + 1] + s_n[sid * 3 + 2] * R[dtd::R_A + 2];
+        double md = 0;
+        for (int q = 0; q < 8; ++q) {
+          double d = -s_c[sid];
+          for (int a = 0; a < 3; ++a) d += s_n[sid * 3 + a] * (((q >> a) & 1) ? ohi[a] : olo[a]);
+          md = std::max(md, std::fabs(d));
+        }
+        // a "rectangle" shifted by |v| <= ypad in y (blur passes) moves its plane by |n_y| |v|
+        if (ypad > 0 && hd.type == DT_SHAPE_RECTANGLE && (hd.flags & DT_F_NAMED_RECT))
+          s_move[sid] = std::fabs(s_n[sid * 3 + 1]) * ypad * (1 + 1e-9) + 1e-12;
+        s_maxd[sid] = 1.02 * md + 1e-3 + s_move[sid];
+        s_plane[sid] = 1;
+      }
+    }
+  }
+  // can no shadow segment from the shading points of cells [c0, c1] (widened box [clo, chi]) to
+  // the light box [llo, lhi] make shape sid's test true? (start-side culling, header)
+  auto start_separated = [&](int sid, const double* clo, const double* chi, const int* c0, const int* c1,
+                             const double* llo, const double* lhi) {
+    if (occ.empty() || !s_plane[sid]) return false;
+    const double* n = s_n.data() + (size_t)sid * 3;
+    const double c = s_c[sid], maxd = s_maxd[sid], mv = s_move[sid];
+    double dlo = INFINITY, dhi = -INFINITY;   // plane distances over the light box
+    for (int q = 0; q < 8; ++q) {
+      double d = -c;
+      for (int a = 0; a < 3; ++a) d += n[a] * (((q >> a) & 1) ? lhi[a] : llo[a]);
+      dlo = std::min(dlo, d);
+      dhi = std::max(dhi, d);
+    }
+    const double s = dlo > 0 ? 1.0 : dhi < 0 ? -1.0 : 0.0;
+    if (s == 0) return false;
+    const double D = (s > 0 ? dlo : -dhi) - mv;
+    if (!(D - 1e-3 > 1e-5 * maxd)) return false;
+    double lmax2 = 0, lmin2 = 0;
+    for (int a = 0; a < 3; ++a) {
+      const double far = std::max(std::fabs(chi[a] - llo[a]), std::fabs(lhi[a] - clo[a]));
+      const double gap = std::max({0.0, llo[a] - chi[a], clo[a] - lhi[a]});
+      lmax2 += far * far;
+      lmin2 += gap * gap;
+    }
+    if (!(lmin2 > 4e-6)) return false;
+    double mn = INFINITY;
+    for (int k = 0; k < 2; ++k) {
+      double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (int z = c0[2]; z <= c1[2]; ++z)
+        for (int y = c0[1]; y <= c1[1]; ++y)
+          for (int x = c0[0]; x <= c1[0]; ++x) {
+            const double* o = occ.data() + (((size_t)z * g.dim[1] + y) * g.dim[0] + x) * 12 + k * 6;
+            for (int a = 0; a < 3; ++a) { blo[a] = std::min(blo[a], o[a]); bhi[a] = std::max(bhi[a], o[3 + a]); }
+          }
+      if (!(blo[0] <= bhi[0] && blo[1] <= bhi[1] && blo[2] <= bhi[2])) continue;   // no such shape here
+      double d = -s * c;
+      for (int a = 0; a < 3; ++a) d += std::min(s * n[a] * blo[a], s * n[a] * bhi[a]);
+      mn = std::min(mn, d - mv - 2 * eta_k[k] * maxd);
+    }
+    const double d_o = std::min(mn, 0.0) + 1e-3 * D / std::sqrt(lmax2);
+    return d_o > 1e-7 * (1 + scale);
+  };
   // DT_SG_ORDER=1: lists ordered likely-occluder first. Opt-in: +0.6% on C3, +1.4 ms host build
   // 
   const char* so = getenv("DT_SG_ORDER");
@@ -565,15 +757,19 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       const int BX = blk_x, BY = blk_y;
       bool have_hull = false;   // shull: the leaf's hull points (empty: a shape without one)
       P3 hint = {0, 0, 0};      // last GJK direction for this leaf (neighbouring cells separate alike)
-      auto separated = [&](const double* clo, const double* chi, int hmode) {
+      long start_n = 0;   // shapes of this test left out by start-side culling alone
+      auto separated = [&](const double* clo, const double* chi, int hmode, const int* c0, const int* c1) {
         bool sep = !shp.empty();
+        start_n = 0;
         for (int sid : shp)
           if (sid != L.shape_index &&
               !shape_separated(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, clo, chi, llo, lhi, mplane, ypad)) {
+            if (start_separated(sid, clo, chi, c0, c1, llo, lhi)) { ++start_n; continue; }
             sep = false;
             break;
           }
         if (sep || hull_cull < hmode) return sep;
+        start_n = 0;
         if (!have_hull) {
           have_hull = true;
           shull.clear();
@@ -605,7 +801,9 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
             double clo[3], chi[3];
             cell_box(xb, yb, z, xe, ye, z, clo, chi);
             if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
-            const bool block_sep = separated(clo, chi, 1);
+            const int b0[3] = {xb, yb, z}, b1[3] = {xe, ye, z};
+            const bool block_sep = separated(clo, chi, 1, b0, b1);
+            const bool block_start = block_sep && start_n > 0;
             for (int y = yb; y <= ye; ++y) {
               const int row = z * g.dim[1] + y;
               if (row < row_lo || row >= row_hi) continue;
@@ -614,7 +812,12 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
                 if (!listed.empty() && listed[cell - band_lo] > max_list) continue;
                 cell_box(x, y, z, x, y, z, clo, chi);
                 if (!swept_meets(clo, chi, llo, lhi, blo, bhi)) continue;
-                if (block_sep || separated(clo, chi, 2)) { ++dropped_n; continue; }
+                const int q0[3] = {x, y, z};
+                if (block_sep || separated(clo, chi, 2, q0, q0)) {
+                  ++dropped_n;
+                  if (block_start || start_n > 0) start_dropped.fetch_add(1, std::memory_order_relaxed);
+                  continue;
+                }
                 pr.push_back({(int32_t)cell, leaf});
                 if (!listed.empty()) ++listed[cell - band_lo];
               }
@@ -881,6 +1084,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
               now_ms() - t_sub);
   }
   g.plane_dropped = dropped;
+  g.start_dropped = start_dropped.load();
   if (timing) fprintf(stderr, "  shadow grid lights: %.2f ms\n", now_ms() - t_setup);
   return g.n_lights > 0;
 }

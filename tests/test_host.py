@@ -461,3 +461,16 @@ def test_block_subtrees_host_build(monkeypatch):
     monkeypatch.setenv("DT_SG_SUB_BLOCK", "4x2")
     c = dt.accel_info(built, g)
     assert c["sg_sub_blocks"] > a["sg_sub_blocks"]
+
+
+def test_shadow_grid_start_side_culling(monkeypatch):
+    """Start-side culling (host_shadowgrid.cpp header) only removes (leaf, cell) pairs: the same
+    cells, tree-walk cells and umbra cells, and at least 4% fewer list entries for C3's room (its
+    back and side walls leave the lists of the cells next to them, for the four ceiling lights),
+    more than 25% fewer for C5 frame 1920's tunnel."""
+    for name, frame, least in (("c3", 240, 0.04), ("c5-1920", 1920, 0.25)):
+        off = _accel(name, frame, 0, {"DT_SG_START": "0"}, monkeypatch)
+        on = _accel(name, frame, 0, {"DT_SG_START": "1"}, monkeypatch)
+        for k in ("sg_cells", "sg_tree_cells", "sg_umbra_cells", "sg_lights"):
+            assert on[k] == off[k], (name, k)
+        assert on["sg_list_entries"] <= (1 - least) * off["sg_list_entries"], (name, on["sg_list_entries"], off["sg_list_entries"])
