@@ -1463,6 +1463,11 @@ __device__ __forceinline__ bool bump_leaf_gathered(const DScene& S, const Walk& 
 #endif
 static_assert(DT_SHAPE_CHECKERBOARD == 6 && DT_SHAPE_CHECKERBOARD_HOLE == 7 && DT_SHAPE_CHECKER_CYLINDER == 8,
               "DT_HAS(6/7/8) below");
+// scattered shadow waves: lanes whose own cell is an umbra cell answer "occluded" without joining
+// the union of the lanes' lists (the coherent path already answered a whole wave so)
+#ifndef DT_UMBRA_LANES
+#define DT_UMBRA_LANES 1
+#endif
 #ifndef DT_SF_CLOSEST
 #define DT_SF_CLOSEST (DT_SHAPE_FIRST && !DT_HAS(6) && !DT_HAS(7) && !DT_HAS(8))
 #endif
@@ -2085,12 +2090,14 @@ __device__ __forceinline__ bool occluded_impl(const DScene& S, const DParams& P,
       bool lin = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.sg_dim[0] && fy < (float)P.sg_dim[1] &&
                  fz < (float)P.sg_dim[2];
       uint32_t loff = 0, ln = 0;
+      bool umb = false;   // the lane's own cell is an umbra cell: every segment from it crosses one face
       if (active && lin) {
         const int cl = ((int)fz * P.sg_dim[1] + (int)fy) * P.sg_dim[0] + (int)fx;
         const uint2 e = ((const uint2*)S.sg_cells)[(size_t)sg_b + cl];
         loff = e.x;
         ln = e.y;
         lin = ln != DT_SG_WALK;
+        umb = DT_UMBRA_LANES && lin && (loff & DT_SG_UMBRA) != 0u;
       }
       DT_CNT(40);
       if (!lin) ln = 0;
@@ -2108,9 +2115,12 @@ __device__ __forceinline__ bool occluded_impl(const DScene& S, const DParams& P,
 #ifdef DT_STAMPS
         cnt.cur_path = 1;
 #endif
+        // lanes in umbra cells are occluded as they are; the rest take the union of their lists
+        const bool rest = active && !umb;
+        if (DT_UMBRA_LANES && !__ballot(rest)) return true;
         if (bump_list)
-          return occluded_union<true, CNT, DT_SHAPE_FIRST>(S, w, active, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt);
-        return occluded_union<false>(S, w, active, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt);
+          return occluded_union<true, CNT, DT_SHAPE_FIRST>(S, w, rest, bstart, sn, sstart, t_max, skip_shape, shift, loff, ln, cnt) || umb;
+        return occluded_union<false>(S, w, rest, bstart, sn, sstart, t_max, skip_shape, 0.0f, loff, ln, cnt) || umb;
       }
 // (bit 3: DT_SHAPE_TRIANGLE is an enum constant, which #if would read as 0; rounds 4-5 had that, so
 // this block was compiled out of the mesh builds)
