@@ -115,10 +115,26 @@ void build_accel(const FlatScene& f, const dt_globals& g, Accel& a, const std::f
   const char* sgv = getenv("DT_SHADOW_GRID");
   const char* sgc = getenv("DT_SG_CELLS");
   const char* sgr = getenv("DT_SG_REACH");
+  // Start-side culling (host_shadowgrid.cpp header), DT_SG_START: 0 off, 2 always, default: a second
+  // build with it when the first one's lists fit (at most 10% of the cells walk the tree). Where the
+  // lists overflow (the C5 transition frames n = 120-139) the shorter lists gain nothing on the
+  // device and the tests cost 30% more host time, in the frame that starts the animation.
+  const char* sgs = getenv("DT_SG_START");
+  const int start_mode = sgs ? atoi(sgs) : 1;
+  const double ypad_main = a.n_bnodes > 0 ? (double)a.bump_pad : 0.0;
   if ((sgv && sgv[0] == '0') || a.no_cull ||
       !build_shadow_grid(dnodes, f, a.sg, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : DT_SG_REACH_DEFAULT,
-                         a.n_bnodes > 0 ? (double)a.bump_pad : 0.0, up_only, g.eye, (double)g.aperture))
+                         ypad_main, up_only, start_mode == 2 ? g.eye : nullptr, (double)g.aperture))
     a.sg = ShadowGrid();
+  else if (start_mode == 1) {
+    size_t walk = 0, cells = a.sg.cells.size() / 2;
+    for (size_t c = 0; c < cells; ++c) walk += a.sg.cells[2 * c + 1] == DT_SG_WALK;
+    ShadowGrid s2;
+    if (walk <= cells / 10 &&
+        build_shadow_grid(dnodes, f, s2, sgc ? atof(sgc) : 32768.0, sgr ? (float)atof(sgr) : DT_SG_REACH_DEFAULT,
+                          ypad_main, up_only, g.eye, (double)g.aperture))
+      a.sg = std::move(s2);
+  }
   for (int l = 0; l < DT_MAX_SGRID; ++l) a.sg.base0[l] = a.sg.base[l];
   // Large blur shifts pad the lists until most cells overflow and walk the tree, pass-0 rays
   // included (C5 frames 1760-1920: 45-70% of the cells). Then an unpadded grid for the pass-0 rays

@@ -62,19 +62,24 @@
 // bound of d(p) over the shading points p that use the cell's list: the points of the widened
 // cell box that some closest-hit test reported. Such a p = start + t_f ray has an exact
 // counterpart X* = start + t* ray on (or, for a near miss of the float tests, within rho of) the
-// shape's box, with |t_f - t*| <= eta |t*|: eta 1e-6 for the plane tests (rectangles,
-// checkerboards, prism faces: a float ratio of a double numerator, ~1.2e-7), 4e-3 for the float
-// quadratics of spheres and cylinders near tangency (sqrt(2^-24) ~ 2.4e-4) and for triangles. So
-// |d(p) - d(X*)| <= eta |d(X*) - d(start)| <= 2 eta maxdist, where maxdist bounds |d| over every
-// ray origin (the root box and the camera's eye region, 2% more for the origins of secondary rays
-// off the hit points), and p lies within eta times the origin box's diagonal of X*, and within 1e-3 of the start o from
-// which the device picks the cell (pad: the sum, + 1e-3). Per cell
-// and class (plane tests / quadratics) the host keeps the bounding box of {shape box + rho} ^ {cell
-// box + pad} over the shapes that meet it; d's minimum over those boxes, less 2 eta maxdist, is
-// the bound. A wall is then left out of a cell's list for a light when that bound, plus
+// shape's box, with |t_f - t*| <= eta |t*|. Class 0, eta 1e-6: the plane tests (rectangles,
+// checkerboards, prism faces: a float ratio of a double numerator, ~1.2e-7) and triangles (a
+// double product with a float 1/det, ~2e-7). Class 1, eta 2e-3: the float quadratics of spheres
+// and cylinders, whose coefficients A, B, C are each rounded once (u = 2^-24) and whose
+// discriminant is formed in double: |d disc| <= 2u B^2 + 2u |4AC| + u |disc| ~ 4u B^2 at tangency,
+// so the root moves by sqrt(4u) |B| / 2A ~ 4.9e-4 t (a near miss of the true surface lands at the
+// ray's closest approach by the same bound); 2e-3 leaves a factor 4. So |d(p) - d(X*)| <=
+// eta |d(X*) - d(start)| <= 2 eta maxdist, where maxdist bounds |d| over every ray origin (the
+// root box and the camera's eye region, 2% more for the origins of secondary rays off the hit
+// points), and p lies within eta times the origin box's diagonal of X*, and within 1e-3 of the
+// start o from which the device picks the cell (pad: the sum, + 1e-3). Per cell and class the
+// host keeps the bounding box of {shape box + rho} ^ {cell box + pad} over the shapes that meet
+// it (and per aligned 8x4x1 block, the union, for the tests on blocks of cells); d's minimum over
+// those boxes, less 2 eta maxdist, is the bound. A wall is then left out of a cell's list for a light when that bound, plus
 // 1e-3 D / Lmax, stays above 1e-7 (1 + scale), D - 1e-3 above 1e-5 maxdist, and the cell box
 // keeps 2e-3 from the light box. The origin box is recorded: a render whose camera's eye region
-// leaves it walks the trees (dt_api.cpp prepare_render). Only axis-aligned planes profit (a tilted
+// leaves it walks the trees (dt_api.cpp prepare_render). host_accel.cpp builds the lists with it
+// only where they fit (DT_SG_START). Only axis-aligned planes profit (a tilted
 // shape's box is not flat), and only rectangles and checkerboards are tried as the culled shape.
 // With ypad > 0 (blur passes) every "rectangle" moves by up to ypad in y: its box grows by ypad in
 // y, and as the culled shape its plane moves by |n_y| ypad (nothing for a wall with a horizontal
@@ -337,15 +342,24 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   long dropped = 0;
   std::atomic<long> start_dropped(0);
   const bool timing = getenv("DT_TIMING") != nullptr;
-  // start-side culling (header); DT_SG_START=0 disables it
-  const char* sg_start_env = getenv("DT_SG_START");
-  const bool start_on = cam != nullptr && !(sg_start_env && sg_start_env[0] == '0');
+  // start-side culling (header): on when the caller passes the camera (host_accel.cpp decides)
+  const bool start_on = cam != nullptr;
   const size_t nshape = fs.hdr.size();
   const int ncell_all = g.dim[0] * g.dim[1] * g.dim[2];
-  const double eta_k[2] = {1e-6, 4e-3};   // plane tests; quadratics and triangles
+  const double eta_k[2] = {1e-6, 2e-3};   // plane and triangle tests; quadratics
   std::vector<double> occ;                 // per cell and class: box (lo[3], hi[3]) of possible shading points
-  std::vector<int8_t> s_plane;             // shapes tried as the culled one: 1 (unit normal in s_n, offset s_c)
-  std::vector<double> s_n, s_c, s_maxd, s_move;
+  std::vector<int8_t> s_plane;             // shapes tried as the culled one: 1 axis-aligned, 2 tilted (record in sp)
+  // per shape tried as the culled one (start-side culling): plane, bounds and, per light, the side
+  // and distance of the light box; one record per shape, so that a test touches few cache lines
+  struct SPlane {
+    double n[3], c, maxd, move;
+    double sD[DT_MAX_SGRID];   // side * D per light (0: the light box is not on one side with margin)
+    double box[6];             // tilted planes: the shape's own box (prefilter)
+  };
+  std::vector<SPlane> sp;
+  const int OB = 8, OB2 = 4;               // occ per aligned block of cells (bocc)
+  int ob_nx = 0, ob_ny = 0;
+  std::vector<double> bocc;
   if (start_on) {
     double olo[3], ohi[3];
     for (int a = 0; a < 3; ++a) {
@@ -360,11 +374,22 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
     occ.assign((size_t)ncell_all * 12, 0.0);
     for (size_t c = 0; c < (size_t)ncell_all * 2; ++c)
       for (int a = 0; a < 3; ++a) { occ[c * 6 + a] = INFINITY; occ[c * 6 + 3 + a] = -INFINITY; }
+    ob_nx = (g.dim[0] + OB - 1) / OB;
+    ob_ny = (g.dim[1] + OB2 - 1) / OB2;
+    bocc.assign((size_t)ob_nx * ob_ny * g.dim[2] * 12, 0.0);
+    for (size_t c = 0; c < bocc.size() / 6; ++c)
+      for (int a = 0; a < 3; ++a) { bocc[c * 6 + a] = INFINITY; bocc[c * 6 + 3 + a] = -INFINITY; }
+    // each shape's box (+ rho) and class, then the cells' boxes, on threads by z-slabs of cells
+    struct SBox { double lo[3], hi[3], pad; int k; };
+    std::vector<SBox> sbox;
+    bool bounded = true;
     std::vector<P3> pts;
-    for (size_t sid = 0; sid < nshape; ++sid) {
+    for (size_t sid = 0; sid < nshape && bounded; ++sid) {
       const dtd::DShapeHdr& hd = fs.hdr[sid];
       const double* gp = fs.geom.data() + hd.off;
-      double blo[3], bhi[3];
+      SBox b;
+      double* blo = b.lo;
+      double* bhi = b.hi;
       int k = 1;
       pts.clear();
       if (hd.type == DT_SHAPE_SPHERE) {
@@ -377,12 +402,12 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
           bhi[a] = std::max(gp[dtd::CY_C1 + a], gp[dtd::CY_C2 + a]) + r;
         }
       } else if (shape_hull_points(hd, gp, 0.0, pts) && !pts.empty()) {
-        k = (hd.type == DT_SHAPE_TRIANGLE) ? 1 : 0;
+        k = 0;
         for (int a = 0; a < 3; ++a) { blo[a] = INFINITY; bhi[a] = -INFINITY; }
         for (const P3& q : pts)
           for (int a = 0; a < 3; ++a) { blo[a] = std::min(blo[a], q[a]); bhi[a] = std::max(bhi[a], q[a]); }
       } else {   // a shape type without bounds here: nothing is start-culled
-        occ.clear();
+        bounded = false;
         break;
       }
       if (ypad > 0 && hd.type == DT_SHAPE_RECTANGLE && (hd.flags & DT_F_NAMED_RECT)) {   // moves in the blur passes
@@ -392,40 +417,65 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       double sd = 0;
       for (int a = 0; a < 3; ++a) sd += (bhi[a] - blo[a]) * (bhi[a] - blo[a]);
       const double rho = 1e-6 * (1 + std::sqrt(sd));
-      // + 2e-3: the device picks the cell from o = p + 1e-3 sn, not from p
-      const double pad = eta_k[k] * diag + 2e-3;
       for (int a = 0; a < 3; ++a) { blo[a] -= rho; bhi[a] += rho; }
-      int i0[3], i1[3];
-      bool any = true;
-      for (int a = 0; a < 3; ++a) {
-        // cells whose widened box [lo + i h - m1, lo + (i + 1) h + m1] meets [blo - pad, bhi + pad]
-        i0[a] = std::max(0, (int)std::ceil((blo[a] - pad - m1 - lo[a]) / hh[a] - 1) - 1);
-        i1[a] = std::min(g.dim[a] - 1, (int)std::floor((bhi[a] + pad + m1 - lo[a]) / hh[a]) + 1);
-        if (i0[a] > i1[a]) any = false;
-      }
-      if (!any) continue;
-      for (int z = i0[2]; z <= i1[2]; ++z)
-        for (int y = i0[1]; y <= i1[1]; ++y)
-          for (int x = i0[0]; x <= i1[0]; ++x) {
-            const int ci[3] = {x, y, z};
-            double clo[3], chi[3];
-            bool meet = true;
-            for (int a = 0; a < 3; ++a) {
-              clo[a] = std::max(blo[a], lo[a] + ci[a] * hh[a] - m1 - pad);
-              chi[a] = std::min(bhi[a], lo[a] + (ci[a] + 1) * hh[a] + m1 + pad);
-              if (clo[a] > chi[a]) meet = false;
+      // + 2e-3: the device picks the cell from o = p + 1e-3 sn, not from p
+      b.pad = eta_k[k] * diag + 2e-3;
+      b.k = k;
+      sbox.push_back(b);
+    }
+    if (!bounded) occ.clear();
+    auto occ_slab = [&](int z_lo, int z_hi) {
+      for (const SBox& b : sbox) {
+        int i0[3], i1[3];
+        bool any = true;
+        for (int a = 0; a < 3; ++a) {
+          // cells whose widened box [lo + i h - m1, lo + (i + 1) h + m1] meets [blo - pad, bhi + pad]
+          i0[a] = std::max(0, (int)std::ceil((b.lo[a] - b.pad - m1 - lo[a]) / hh[a] - 1) - 1);
+          i1[a] = std::min(g.dim[a] - 1, (int)std::floor((b.hi[a] + b.pad + m1 - lo[a]) / hh[a]) + 1);
+          if (i0[a] > i1[a]) any = false;
+        }
+        i0[2] = std::max(i0[2], z_lo);
+        i1[2] = std::min(i1[2], z_hi - 1);
+        if (!any || i0[2] > i1[2]) continue;
+        for (int z = i0[2]; z <= i1[2]; ++z)
+          for (int y = i0[1]; y <= i1[1]; ++y)
+            for (int x = i0[0]; x <= i1[0]; ++x) {
+              const int ci[3] = {x, y, z};
+              double clo[3], chi[3];
+              bool meet = true;
+              for (int a = 0; a < 3; ++a) {
+                clo[a] = std::max(b.lo[a], lo[a] + ci[a] * hh[a] - m1 - b.pad);
+                chi[a] = std::min(b.hi[a], lo[a] + (ci[a] + 1) * hh[a] + m1 + b.pad);
+                if (clo[a] > chi[a]) meet = false;
+              }
+              if (!meet) continue;
+              double* o = occ.data() + (((size_t)z * g.dim[1] + y) * g.dim[0] + x) * 12 + b.k * 6;
+              for (int a = 0; a < 3; ++a) { o[a] = std::min(o[a], clo[a]); o[3 + a] = std::max(o[3 + a], chi[a]); }
             }
-            if (!meet) continue;
-            double* o = occ.data() + (((size_t)z * g.dim[1] + y) * g.dim[0] + x) * 12 + k * 6;
-            for (int a = 0; a < 3; ++a) { o[a] = std::min(o[a], clo[a]); o[3 + a] = std::max(o[3 + a], chi[a]); }
+      }
+    };
+    if (!occ.empty()) {
+      const int nt = std::max(1, std::min({(int)std::thread::hardware_concurrency(), 16, g.dim[2]}));
+      std::vector<std::thread> th;
+      for (int t = 1; t < nt; ++t) th.emplace_back(occ_slab, g.dim[2] * t / nt, g.dim[2] * (t + 1) / nt);
+      occ_slab(0, g.dim[2] / nt);
+      for (auto& t : th) t.join();
+      // the same per aligned block of OB x OB2 x 1 cells (range queries: the blocks covering them)
+      for (int z = 0; z < g.dim[2]; ++z)
+        for (int y = 0; y < g.dim[1]; ++y)
+          for (int x = 0; x < g.dim[0]; ++x) {
+            const double* o = occ.data() + (((size_t)z * g.dim[1] + y) * g.dim[0] + x) * 12;
+            double* q = bocc.data() + (((size_t)z * ob_ny + y / OB2) * ob_nx + x / OB) * 12;
+            for (int k = 0; k < 2; ++k)
+              for (int a = 0; a < 3; ++a) {
+                q[k * 6 + a] = std::min(q[k * 6 + a], o[k * 6 + a]);
+                q[k * 6 + 3 + a] = std::max(q[k * 6 + 3 + a], o[k * 6 + 3 + a]);
+              }
           }
     }
     if (!occ.empty()) {
       s_plane.assign(nshape, 0);
-      s_n.assign(nshape * 3, 0.0);
-      s_c.assign(nshape, 0.0);
-      s_maxd.assign(nshape, 0.0);
-      s_move.assign(nshape, 0.0);
+      sp.assign(nshape, SPlane());
       for (size_t sid = 0; sid < nshape; ++sid) {
         const dtd::DShapeHdr& hd = fs.hdr[sid];
         const double* R = nullptr;
@@ -435,40 +485,49 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
         const double* n = R + dtd::R_N;
         const double nn = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
         if (!(nn > 0) || !std::isfinite(nn)) continue;
-        for (int a = 0; a < 3; ++a) s_n[sid * 3 + a] = n[a] / nn;
-        s_c[sid] = s_n[sid * 3] * R[dtd::R_A] + s_n[sid * 3 + 1] * R[dtd::R_A + 1] + s_n[sid * 3 + 2] * R[dtd::R_A + 2];
+        SPlane& P = sp[sid];
+        for (int a = 0; a < 3; ++a) P.n[a] = n[a] / nn;
+        P.c = P.n[0] * R[dtd::R_A] + P.n[1] * R[dtd::R_A + 1] + P.n[2] * R[dtd::R_A + 2];
         double md = 0;
         for (int q = 0; q < 8; ++q) {
-          double d = -s_c[sid];
-          for (int a = 0; a < 3; ++a) d += s_n[sid * 3 + a] * (((q >> a) & 1) ? ohi[a] : olo[a]);
+          double d = -P.c;
+          for (int a = 0; a < 3; ++a) d += P.n[a] * (((q >> a) & 1) ? ohi[a] : olo[a]);
           md = std::max(md, std::fabs(d));
         }
         // a "rectangle" shifted by |v| <= ypad in y (blur passes) moves its plane by |n_y| |v|
-        if (ypad > 0 && hd.type == DT_SHAPE_RECTANGLE && (hd.flags & DT_F_NAMED_RECT))
-          s_move[sid] = std::fabs(s_n[sid * 3 + 1]) * ypad * (1 + 1e-9) + 1e-12;
-        s_maxd[sid] = 1.02 * md + 1e-3 + s_move[sid];
+        P.move = (ypad > 0 && hd.type == DT_SHAPE_RECTANGLE && (hd.flags & DT_F_NAMED_RECT))
+                     ? std::fabs(P.n[1]) * ypad * (1 + 1e-9) + 1e-12 : 0.0;
+        P.maxd = 1.02 * md + 1e-3 + P.move;
         s_plane[sid] = 1;
+        int zeros = 0;
+        for (int a = 0; a < 3; ++a) zeros += P.n[a] == 0.0;
+        if (zeros < 2) {   // a tilted plane: its own box is not flat (prefilter below)
+          s_plane[sid] = 2;
+          for (int a = 0; a < 3; ++a) { P.box[a] = sbox[sid].lo[a]; P.box[3 + a] = sbox[sid].hi[a]; }
+        }
       }
     }
   }
+  // per (shape, light): the light box's side of the shape's plane (+-1, 0: both) and D, its
+  // distance from the plane less the plane's blur movement (filled once the light boxes are known)
   // can no shadow segment from the shading points of cells [c0, c1] (widened box [clo, chi]) to
-  // the light box [llo, lhi] make shape sid's test true? (start-side culling, header)
-  auto start_separated = [&](int sid, const double* clo, const double* chi, const int* c0, const int* c1,
+  // light l's box [llo, lhi] make shape sid's test true? (start-side culling, header)
+  auto start_separated = [&](int sid, size_t l, const double* clo, const double* chi, const int* c0, const int* c1,
                              const double* llo, const double* lhi) {
     if (occ.empty() || !s_plane[sid]) return false;
-    const double* n = s_n.data() + (size_t)sid * 3;
-    const double c = s_c[sid], maxd = s_maxd[sid], mv = s_move[sid];
-    double dlo = INFINITY, dhi = -INFINITY;   // plane distances over the light box
-    for (int q = 0; q < 8; ++q) {
-      double d = -c;
-      for (int a = 0; a < 3; ++a) d += n[a] * (((q >> a) & 1) ? lhi[a] : llo[a]);
-      dlo = std::min(dlo, d);
-      dhi = std::max(dhi, d);
+    const SPlane& P = sp[sid];
+    const double sD = P.sD[l];
+    if (sD == 0) return false;
+    const double s = sD > 0 ? 1.0 : -1.0, D = std::fabs(sD);
+    // a tilted plane whose own box meets the cells: the box's corners leave the plane by far more
+    // than the margin, so the bound fails (a host-time prefilter; it only keeps leaves)
+    if (s_plane[sid] == 2) {
+      const double* b = P.box;
+      if (b[0] <= chi[0] && b[3] >= clo[0] && b[1] <= chi[1] && b[4] >= clo[1] && b[2] <= chi[2] && b[5] >= clo[2])
+        return false;
     }
-    const double s = dlo > 0 ? 1.0 : dhi < 0 ? -1.0 : 0.0;
-    if (s == 0) return false;
-    const double D = (s > 0 ? dlo : -dhi) - mv;
-    if (!(D - 1e-3 > 1e-5 * maxd)) return false;
+    const double* n = P.n;
+    const double c = P.c, maxd = P.maxd, mv = P.move;
     double lmax2 = 0, lmin2 = 0;
     for (int a = 0; a < 3; ++a) {
       const double far = std::max(std::fabs(chi[a] - llo[a]), std::fabs(lhi[a] - clo[a]));
@@ -477,15 +536,23 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       lmin2 += gap * gap;
     }
     if (!(lmin2 > 4e-6)) return false;
+    // the cells' boxes of possible shading points: the cell's own, or the aligned blocks covering
+    // the range (a superset: the bound can only be lower)
+    const bool one = c0[0] == c1[0] && c0[1] == c1[1] && c0[2] == c1[2];
     double mn = INFINITY;
     for (int k = 0; k < 2; ++k) {
       double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
-      for (int z = c0[2]; z <= c1[2]; ++z)
-        for (int y = c0[1]; y <= c1[1]; ++y)
-          for (int x = c0[0]; x <= c1[0]; ++x) {
-            const double* o = occ.data() + (((size_t)z * g.dim[1] + y) * g.dim[0] + x) * 12 + k * 6;
-            for (int a = 0; a < 3; ++a) { blo[a] = std::min(blo[a], o[a]); bhi[a] = std::max(bhi[a], o[3 + a]); }
-          }
+      auto take = [&](const double* o) {
+        for (int a = 0; a < 3; ++a) { blo[a] = std::min(blo[a], o[a]); bhi[a] = std::max(bhi[a], o[3 + a]); }
+      };
+      if (one) {
+        take(occ.data() + (((size_t)c0[2] * g.dim[1] + c0[1]) * g.dim[0] + c0[0]) * 12 + k * 6);
+      } else {
+        for (int z = c0[2]; z <= c1[2]; ++z)
+          for (int by = c0[1] / OB2; by <= c1[1] / OB2; ++by)
+            for (int bx = c0[0] / OB; bx <= c1[0] / OB; ++bx)
+              take(bocc.data() + (((size_t)z * ob_ny + by) * ob_nx + bx) * 12 + k * 6);
+      }
       if (!(blo[0] <= bhi[0] && blo[1] <= bhi[1] && blo[2] <= bhi[2])) continue;   // no such shape here
       double d = -s * c;
       for (int a = 0; a < 3; ++a) d += std::min(s * n[a] * blo[a], s * n[a] * bhi[a]);
@@ -670,6 +737,27 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       if (qmn > S.mud || qmx < -S.mud) S.fl.push_back((int)fi);
     }
   }
+  if (!occ.empty()) {   // start-side culling: each plane's side of each light box
+    for (size_t sid = 0; sid < nshape; ++sid) {
+      if (!s_plane[sid]) continue;
+      SPlane& P = sp[sid];
+      for (size_t l = 0; l < nl; ++l) {
+        P.sD[l] = 0;
+        if (!ls[l].on) continue;
+        double dlo = INFINITY, dhi = -INFINITY;
+        for (int q = 0; q < 8; ++q) {
+          double d = -P.c;
+          for (int a = 0; a < 3; ++a) d += P.n[a] * (((q >> a) & 1) ? ls[l].lhi[a] : ls[l].llo[a]);
+          dlo = std::min(dlo, d);
+          dhi = std::max(dhi, d);
+        }
+        const int side = dlo > 0 ? 1 : dhi < 0 ? -1 : 0;
+        const double D = (side > 0 ? dlo : -dhi) - P.move;
+        // the far end's margin (header): D - 1e-3 above 1e-5 maxdist
+        if (side != 0 && D - 1e-3 > 1e-5 * P.maxd) P.sD[l] = side * D;
+      }
+    }
+  }
   // umbra cells of light l, rows of blocks (BX x BY x 1 cells) t, t + nt, ...: every cell tries
   // the faces in the same order, so the result does not depend on the partition
   const int UBX = std::max(1, blk_x), UBY = std::max(1, blk_y);
@@ -764,7 +852,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
         for (int sid : shp)
           if (sid != L.shape_index &&
               !shape_separated(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, clo, chi, llo, lhi, mplane, ypad)) {
-            if (start_separated(sid, clo, chi, c0, c1, llo, lhi)) { ++start_n; continue; }
+            if (start_separated(sid, l, clo, chi, c0, c1, llo, lhi)) { ++start_n; continue; }
             sep = false;
             break;
           }

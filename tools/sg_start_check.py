@@ -1,7 +1,9 @@
 """Bit-identity of start-side culling (host_shadowgrid.cpp header): every case is rendered twice on
-the GPU, from a scene whose shadow-grid lists were built with DT_SG_START=0 and one built with the
-default (start-side culling on), and the two images, ray counts and shadow-ray counts must agree
-exactly. The lists are host data, so any difference in what the device tests would show up here.
+the GPU, from a scene whose shadow-grid lists were built with DT_SG_START=0 and one built with
+DT_SG_START=2 (start-side culling on every frame, the overflowing transition frames included;
+SG_START_MODE=1 checks the default, which skips those), and the two images, ray counts and
+shadow-ray counts must agree exactly. The lists are host data, so any difference in what the device
+tests would show up here.
 
     python tools/sg_start_check.py [case ...]      (default: all; prints one line per case)
 """
@@ -39,7 +41,7 @@ def main():
         built = dt.build_scene("final", frame, g)
         g.xRes, g.yRes, g.antialias_samples, g.max_depth = W, H, spp, depth
         res = []
-        for env in ("0", "1"):
+        for env in ("0", os.environ.get("SG_START_MODE", "2")):
             os.environ["DT_SG_START"] = env
             info = dt.accel_info(built, g)
             scene = dt.Scene(built, g)
