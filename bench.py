@@ -230,8 +230,10 @@ def load_pmc_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    # 10 timed frames (0.33 s of C3): with two frames in flight the first launch runs alone, which
+    # 3 steps weighed at ~1% of the frame time (profiles/r06fa_bench.json against r06fa_torchrun_n1.json)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frac", type=int, default=8, help="CPU baseline renders 1/N of the tiles")
