@@ -30,8 +30,14 @@
 // t_max) and inside the shape up to the f32 rounding of its checks, far inside the margin. GJK
 // proposes the direction; the separation is then checked exactly along it (the gap between the
 // two hulls' projections), so a poorly converged GJK can only keep a leaf, never drop one.
-// Cylinders and spheres are never hull-culled (their float quadratic roots near tangency err by
-// more than the margin).
+// Spheres and cylinders (round 6) are hull-culled by their axis segment (a point for a sphere):
+// the reference's f32 quadratic reports a hit only at a point of the ray within r + delta of the
+// axis and inside the axial range (the range check runs on that point), where the discriminant's
+// roundings (coefficients rounded once, ~4u B^2) admit a false hit out to
+// r + 2u |start - axis|^2 / r and move a true one along the ray by ~sqrt(4u) t, i.e. off the
+// surface by ~u t^2 / 2r; delta = 1e-3 + 1e-6 (1 + L^2 / r), L bounding |point - axis end| over
+// the hull, covers both with a factor of 8. The segment's points lie in the hull, so a hull that
+// keeps r + delta + the usual margin from the axis segment sees no hit (DT_SG_QUAD=0: off).
 //
 // Umbra cells: a cell all of whose segments to the light cross the inside of one fixed planar
 // face (a rectangle that is not a moving "rectangle", a checkerboard without hole, a prism face)
@@ -569,6 +575,9 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   // single cells (C5 tunnel frames: -46% kernel time with 1, 1% more with 2, for 3x the host time)
   const char* sh = getenv("DT_SG_HULL");
   const int hull_cull = sh ? atoi(sh) : 1;
+  // DT_SG_QUAD=0: spheres and cylinders keep their leaves out of hull culling (before round 6)
+  const char* sq = getenv("DT_SG_QUAD");
+  const bool quad_hull = !(sq && sq[0] == '0');
   // DT_SG_MAX_LIST: cells with longer lists walk the tree instead (default DT_SGRID_MAX_LIST)
   const char* mls = getenv("DT_SG_MAX_LIST");
   const int max_list = mls && atoi(mls) > 0 ? atoi(mls) : DT_SGRID_MAX_LIST;
@@ -826,6 +835,8 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
     const std::vector<P3>& lhull = S.lhull;
     std::vector<int> shp;
     std::vector<P3> shull, hA(8 + lhull.size());
+    struct Quad { P3 a, b; double r; };
+    std::vector<Quad> squad;
     for (size_t k = 0; k < lhull.size(); ++k) hA[8 + k] = lhull[k];
     for (int leaf : leaves) {
       const dtd::DNodeDev& nd = nodes[leaf];
@@ -843,7 +854,9 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       // block, the same holds for every cell in it. The lists come out as from per-cell tests
       // (the margins m1 and mplane lie far above the rounding of the box corners).
       const int BX = blk_x, BY = blk_y;
-      bool have_hull = false;   // shull: the leaf's hull points (empty: a shape without one)
+      bool have_hull = false;   // shull: the leaf's planar hull points; squad: its spheres and cylinders
+      bool hull_ok = false;     // every shape of the leaf is planar, a sphere or a cylinder
+      P3 qhint = {0, 0, 0};
       P3 hint = {0, 0, 0};      // last GJK direction for this leaf (neighbouring cells separate alike)
       long start_n = 0;   // shapes of this test left out by start-side culling alone
       auto separated = [&](const double* clo, const double* chi, int hmode, const int* c0, const int* c1) {
@@ -860,17 +873,49 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
         start_n = 0;
         if (!have_hull) {
           have_hull = true;
+          hull_ok = true;
           shull.clear();
-          for (int sid : shp)
-            if (sid != L.shape_index &&
-                !shape_hull_points(fs.hdr[sid], fs.geom.data() + fs.hdr[sid].off, ypad, shull, up_only)) {
-              shull.clear();
+          squad.clear();
+          for (int sid : shp) {
+            if (sid == L.shape_index) continue;
+            const dtd::DShapeHdr& hd = fs.hdr[sid];
+            const double* gp = fs.geom.data() + hd.off;
+            if (shape_hull_points(hd, gp, ypad, shull, up_only)) continue;
+            // spheres and cylinders: their axis (a point for a sphere) and radius (header, "Hull
+            // culling"); they do not move in the blur passes
+            Quad q;
+            if (hd.type == DT_SHAPE_SPHERE && quad_hull) {
+              q.a = {gp[dtd::SP_C], gp[dtd::SP_C + 1], gp[dtd::SP_C + 2]};
+              q.b = q.a;
+              q.r = std::sqrt(gp[dtd::SP_R2]);
+            } else if (!quad_hull) {
+              hull_ok = false;
+              break;
+            } else if (hd.type == DT_SHAPE_CYLINDER || hd.type == DT_SHAPE_CHECKER_CYLINDER) {
+              q.a = {gp[dtd::CY_C1], gp[dtd::CY_C1 + 1], gp[dtd::CY_C1 + 2]};
+              q.b = {gp[dtd::CY_C2], gp[dtd::CY_C2 + 1], gp[dtd::CY_C2 + 2]};
+              q.r = std::sqrt(gp[dtd::CY_R2]);
+            } else {
+              hull_ok = false;
               break;
             }
+            if (!(q.r > 0) || !std::isfinite(q.r)) { hull_ok = false; break; }
+            squad.push_back(q);
+          }
         }
-        if (shull.empty()) return false;
+        if (!hull_ok || (shull.empty() && squad.empty())) return false;
         for (int k = 0; k < 8; ++k) hA[k] = {(k & 1) ? chi[0] : clo[0], (k & 2) ? chi[1] : clo[1], (k & 4) ? chi[2] : clo[2]};
-        return hulls_separated(hA.data(), (int)hA.size(), shull.data(), (int)shull.size(), m2 + mplane, hint);
+        if (!shull.empty() && !hulls_separated(hA.data(), (int)hA.size(), shull.data(), (int)shull.size(), m2 + mplane, hint))
+          return false;
+        for (const Quad& q : squad) {
+          double L = 0;
+          for (const P3& h : hA) L = std::max(L, std::sqrt(dot3(sub3(h, q.a), sub3(h, q.a))));
+          L += std::sqrt(dot3(sub3(q.b, q.a), sub3(q.b, q.a)));
+          const P3 seg[2] = {q.a, q.b};
+          const double m = q.r + 1e-3 + 1e-6 * (1 + L * L / q.r) + m2 + mplane;
+          if (!hulls_separated(hA.data(), (int)hA.size(), seg, 2, m, qhint)) return false;
+        }
+        return true;
       };
       auto cell_box = [&](int x0, int y0, int z0, int x1, int y1, int z1, double* clo, double* chi) {
         const int c0[3] = {x0, y0, z0}, c1[3] = {x1, y1, z1};

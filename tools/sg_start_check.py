@@ -1,6 +1,7 @@
 """Bit-identity of start-side culling (host_shadowgrid.cpp header): every case is rendered twice on
-the GPU, from a scene whose shadow-grid lists were built with DT_SG_START=0 and one built with
-DT_SG_START=2 (start-side culling on every frame, the overflowing transition frames included;
+the GPU, from a scene whose shadow-grid lists were built as before round 6 (DT_SG_START=0,
+DT_SG_QUAD=0: no start-side culling, no hull culling of sphere and cylinder leaves) and one built
+with both (DT_SG_START=2: start-side culling on every frame, the overflowing transition frames included;
 SG_START_MODE=1 checks the default, which skips those), and the two images, ray counts and
 shadow-ray counts must agree exactly. The lists are host data, so any difference in what the device
 tests would show up here.
@@ -43,6 +44,7 @@ def main():
         res = []
         for env in ("0", os.environ.get("SG_START_MODE", "2")):
             os.environ["DT_SG_START"] = env
+            os.environ["DT_SG_QUAD"] = "0" if env == "0" else "1"   # the baseline: lists before round 6
             info = dt.accel_info(built, g)
             scene = dt.Scene(built, g)
             out = torch.zeros(3 * W * H, dtype=torch.float32, device="cuda")
@@ -50,6 +52,7 @@ def main():
             res.append((out.cpu().numpy(), st, info["sg_list_entries"]))
             scene.close()
         os.environ.pop("DT_SG_START", None)
+        os.environ.pop("DT_SG_QUAD", None)
         (a, sa, ea), (b, sb, eb) = res
         same = np.array_equal(a.view(np.uint32), b.view(np.uint32)) and sa.rays == sb.rays and sa.shadow_rays == sb.shadow_rays
         bad += not same
