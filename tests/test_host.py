@@ -474,3 +474,15 @@ def test_shadow_grid_start_side_culling(monkeypatch):
         for k in ("sg_cells", "sg_tree_cells", "sg_umbra_cells", "sg_lights"):
             assert on[k] == off[k], (name, k)
         assert on["sg_list_entries"] <= (1 - least) * off["sg_list_entries"], (name, on["sg_list_entries"], off["sg_list_entries"])
+
+
+def test_shadow_grid_quadric_hull_culling(monkeypatch):
+    """Hull culling of sphere and cylinder leaves (host_shadowgrid.cpp header, round 6) only
+    removes (leaf, cell) pairs: the same cells, tree-walk cells and umbra cells; C5 frame 1920's
+    tunnel (cylinder columns) loses at least 10% of its list entries, C3's room at least 1%."""
+    for name, frame, least in (("c3", 240, 0.01), ("c5-1920", 1920, 0.10)):
+        off = _accel(name, frame, 0, {"DT_SG_START": "0", "DT_SG_QUAD": "0"}, monkeypatch)
+        on = _accel(name, frame, 0, {"DT_SG_START": "0", "DT_SG_QUAD": "1"}, monkeypatch)
+        for k in ("sg_cells", "sg_tree_cells", "sg_umbra_cells", "sg_lights"):
+            assert on[k] == off[k], (name, k)
+        assert on["sg_list_entries"] <= (1 - least) * off["sg_list_entries"], (name, on["sg_list_entries"], off["sg_list_entries"])
