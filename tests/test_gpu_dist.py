@@ -38,12 +38,12 @@ def _free_port():
     return p
 
 
-def _globals():
+def _globals(spp=16, W=400, H=300):
     g = dt.globals_default()
     g.use_model = 0
     built = dt.build_scene("final", 240, g)
     # C2's settings (Cook-Torrance doors, area-light soft shadows, glossy) at a quarter of its pixels
-    g.xRes, g.yRes, g.antialias_samples, g.max_depth = 400, 300, 16, 4
+    g.xRes, g.yRes, g.antialias_samples, g.max_depth = W, H, spp, 4
     return g, built
 
 
@@ -134,7 +134,7 @@ class _HostHopSplit:
         self.s.assemble(gathered, image, stream)
 
 
-def _rank_device_path(rank, world, port, outdir):
+def _rank_device_path(rank, world, port, outdir, shape=(16, 400, 300)):
     """bench.py's N > 1 step (bench.py step(): render_async on streams[k % 2] with a scene object per
     stream into device slabs, GatherPipeline.begin / submit / finish, the device scatter on rank 0)."""
     import torch.distributed as dist
@@ -144,7 +144,7 @@ def _rank_device_path(rank, world, port, outdir):
         from distraytracer_amd.multigpu import FrameSplit, GatherPipeline
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        g, built = _globals()
+        g, built = _globals(*shape)
         scenes = [dt.Scene(built, g), dt.Scene(built, g)]
         split = _HostHopSplit(FrameSplit(g, world, rank))
         zd = lambda n: torch.zeros(n, dtype=torch.float32, device=dev)
@@ -175,18 +175,20 @@ def _rank_device_path(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-def test_shipped_device_path_world2(cuda, tmp_path):
+@pytest.mark.parametrize("shape", [(16, 400, 300), (81, 160, 96)], ids=["16spp-8x8", "81spp-2x2-chunks"])
+def test_shipped_device_path_world2(cuda, tmp_path, shape):
     """The N > 1 path as bench.py ships it: two frames in flight per rank on two
     streams with a scene object each, device slabs, GatherPipeline's event ordering, and the device
     scatter (dt_unpack_slabs) on rank 0; only the collective's transport is a host hop over gloo.
     Every assembled frame is bit-identical to a single-process render of that frame, and rank 1's
-    slab of frame 0 equals the oracle's render of its share."""
+    slab of frame 0 equals the oracle's render of its share. At 16 spp the split takes 8x8 tiles; at
+    81 spp (two 64-sample chunks a pixel) 2x2 tiles and chunk items, as C4 does at N > 1."""
     world = 2
-    mp.start_processes(_rank_device_path, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_rank_device_path, args=(world, _free_port(), str(tmp_path), shape), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(tmp_path / "dev_images.npy")
     assert got.shape[0] == FRAMES + 1
-    g, built = _globals()
+    g, built = _globals(*shape)
     scene = dt.Scene(built, g)
     for k in range(FRAMES + 1):
         g.seed = k
