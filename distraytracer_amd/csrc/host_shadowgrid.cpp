@@ -68,29 +68,42 @@
 // bound of d(p) over the shading points p that use the cell's list: the points of the widened
 // cell box that some closest-hit test reported. Such a p = start + t_f ray has an exact
 // counterpart X* = start + t* ray on (or, for a near miss of the float tests, within rho of) the
-// shape's box, with |t_f - t*| <= eta |t*|. Class 0, eta 1e-6: the plane tests (rectangles,
-// checkerboards, prism faces: a float ratio of a double numerator, ~1.2e-7) and triangles (a
-// double product with a float 1/det, ~2e-7). Class 1, eta 2e-3: the float quadratics of spheres
+// shape's box, with |t_f - t*| <= eta |t*|. Class 0, eta 1.25e-7: the plane test of a rectangle
+// or checkerboard whose box is flat in one axis. Its normal is that axis exactly (two exact zeros
+// in the cross product of two edges, normalised to +-1), so num = (A - start).n is one rounded
+// difference and dn = (float)(ray.n) one rounding of an exact product: t_f = t* (1 + e1)(1 + e3) /
+// (1 + e2), |e2|, |e3| <= 2^-24, |e1| ~ 2^-53, so |t_f / t* - 1| <= 1.1921e-7; X* lies on the
+// box's plane exactly and a near miss of the float checks leaves the box only within the plane
+// (rho is not added along the flat axis). Class 2, eta 1e-6: every other planar test (tilted
+// planes and prism faces: a float ratio of a double numerator, ~1.2e-7; triangles: a double
+// product with a float 1/det, ~2e-7). Class 1, eta 2e-3: the float quadratics of spheres
 // and cylinders, whose coefficients A, B, C are each rounded once (u = 2^-24) and whose
 // discriminant is formed in double: |d disc| <= 2u B^2 + 2u |4AC| + u |disc| ~ 4u B^2 at tangency,
 // so the root moves by sqrt(4u) |B| / 2A ~ 4.9e-4 t (a near miss of the true surface lands at the
 // ray's closest approach by the same bound); 2e-3 leaves a factor 4. So |d(p) - d(X*)| <=
-// eta |d(X*) - d(start)| <= 2 eta maxdist, where maxdist bounds |d| over every ray origin (the
-// root box and the camera's eye region, 2% more for the origins of secondary rays off the hit
-// points), and p lies within eta times the origin box's diagonal of X*, and within 1e-3 of the
-// start o from which the device picks the cell (pad: the sum, + 1e-3). Per cell and class the
-// host keeps the bounding box of {shape box + rho} ^ {cell box + pad} over the shapes that meet
-// it (and per aligned 8x4x1 block, the union, for the tests on blocks of cells); d's minimum over
-// those boxes, less 2 eta maxdist, is the bound. A wall is then left out of a cell's list for a light when that bound, plus
-// 1e-3 D / Lmax, stays above 1e-7 (1 + scale), D - 1e-3 above 1e-5 maxdist, and the cell box
-// keeps 2e-3 from the light box. The origin box is recorded: a render whose camera's eye region
-// leaves it walks the trees (dt_api.cpp prepare_render). host_accel.cpp builds the lists with it
-// only where they fit (DT_SG_START). Only axis-aligned planes profit (a tilted
-// shape's box is not flat), and only rectangles and checkerboards are tried as the culled shape.
+// eta |d(X*) - d(start)|, which is at most eta times the span of d over the box of X* and the box
+// of ray origins. That box (round 6, second version) holds the camera's eye region and, around
+// each shape whose material spawns secondary rays (refl_materials, cpp:574-576), where those rays
+// start: the hit point, within eta |X* - start| of the shape's box, plus 1e-3 times the unit
+// in / refl_ray or a glossy sample_refl (<= 3080 long). It is computed twice, bounding
+// |X* - start| first by the root box's diagonal and then by the first box's; before, it was the
+// root box, which C3's window-frame prisms stretch to y = +-1000. p lies within eta times the
+// diagonal of the origin box and the shape's box of X*, and within 1e-3 of the start o from which
+// the device picks the cell (pad: the sum, + 1e-3). Per cell and class the host keeps the
+// bounding box of {shape box + rho} ^ {cell box + pad} over the shapes that meet it (and per
+// aligned 8x4x1 block, the union, for the tests on blocks of cells); d's minimum over those
+// boxes, less eta times the span, is the bound. A wall is then left out of a cell's list for a
+// light when that bound, plus 1e-3 D / Lmax, stays above 1e-7 (1 + scale), D - 1e-3 above 1e-5
+// maxdist (|d| over the root box and the eye region), and the cell box keeps 2e-3 from the light
+// box. The origin box is recorded: a render whose camera's eye region leaves it walks the trees
+// (dt_api.cpp prepare_render). host_accel.cpp builds the lists with it only where they fit
+// (DT_SG_START). Only axis-aligned planes profit (a tilted shape's box is not flat), and only
+// rectangles and checkerboards are tried as the culled shape.
 // With ypad > 0 (blur passes) every "rectangle" moves by up to ypad in y: its box grows by ypad in
 // y, and as the culled shape its plane moves by |n_y| ypad (nothing for a wall with a horizontal
-// normal), which D and the bound lose. C3: the back and side walls leave the lists of the boundary cells for the four
-// ceiling lights.
+// normal), which D and the bound lose. C3: the ceiling, back and side walls leave the lists of the
+// boundary cells for the four ceiling lights (263802 -> 195500 list entries; 225677 with the root
+// box as the origin box).
 //
 // Motion blur: with ypad > 0 the lists also serve the blur passes (bumped leaf boxes, "rectangle"
 // shapes shifted by |val| <= ypad in y): leaf boxes are padded by ypad in y, and a moving
@@ -352,13 +365,17 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   const bool start_on = cam != nullptr;
   const size_t nshape = fs.hdr.size();
   const int ncell_all = g.dim[0] * g.dim[1] * g.dim[2];
-  const double eta_k[2] = {1e-6, 2e-3};   // plane and triangle tests; quadratics
+  // |t_f - t*| <= eta |t*| per class of closest-hit test (header): 0 axis-aligned plane tests, 1 the
+  // f32 quadratics, 2 every other planar test (tilted planes, triangles)
+  constexpr int NK = 3;
+  const double eta_k[NK] = {1.25e-7, 2e-3, 1e-6};
   std::vector<double> occ;                 // per cell and class: box (lo[3], hi[3]) of possible shading points
   std::vector<int8_t> s_plane;             // shapes tried as the culled one: 1 axis-aligned, 2 tilted (record in sp)
   // per shape tried as the culled one (start-side culling): plane, bounds and, per light, the side
   // and distance of the light box; one record per shape, so that a test touches few cache lines
   struct SPlane {
     double n[3], c, maxd, move;
+    double dblo, dbhi;         // n.x - c over the box of ray origins
     double sD[DT_MAX_SGRID];   // side * D per light (0: the light box is not on one side with margin)
     double box[6];             // tilted planes: the shape's own box (prefilter)
   };
@@ -372,21 +389,19 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       olo[a] = std::min((double)nodes[0].lb[a], cam[a] - cam_r);
       ohi[a] = std::max((double)nodes[0].ub[a], cam[a] + cam_r);
     }
-    g.org_check = true;
-    for (int a = 0; a < 3; ++a) { g.org_lo[a] = olo[a]; g.org_hi[a] = ohi[a]; }
     double diag = 0;
     for (int a = 0; a < 3; ++a) diag += (ohi[a] - olo[a]) * (ohi[a] - olo[a]);
     diag = std::sqrt(diag) * 1.02;
-    occ.assign((size_t)ncell_all * 12, 0.0);
-    for (size_t c = 0; c < (size_t)ncell_all * 2; ++c)
+    occ.assign((size_t)ncell_all * 6 * NK, 0.0);
+    for (size_t c = 0; c < (size_t)ncell_all * NK; ++c)
       for (int a = 0; a < 3; ++a) { occ[c * 6 + a] = INFINITY; occ[c * 6 + 3 + a] = -INFINITY; }
     ob_nx = (g.dim[0] + OB - 1) / OB;
     ob_ny = (g.dim[1] + OB2 - 1) / OB2;
-    bocc.assign((size_t)ob_nx * ob_ny * g.dim[2] * 12, 0.0);
+    bocc.assign((size_t)ob_nx * ob_ny * g.dim[2] * 6 * NK, 0.0);
     for (size_t c = 0; c < bocc.size() / 6; ++c)
       for (int a = 0; a < 3; ++a) { bocc[c * 6 + a] = INFINITY; bocc[c * 6 + 3 + a] = -INFINITY; }
     // each shape's box (+ rho) and class, then the cells' boxes, on threads by z-slabs of cells
-    struct SBox { double lo[3], hi[3], pad; int k; };
+    struct SBox { double lo[3], hi[3], pad; int k; bool refl, glossy; };
     std::vector<SBox> sbox;
     bool bounded = true;
     std::vector<P3> pts;
@@ -397,6 +412,10 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       double* blo = b.lo;
       double* bhi = b.hi;
       int k = 1;
+      const int mt = fs.mat[sid].material;
+      b.refl = mt == DT_MAT_GLASS || mt == DT_MAT_STEEL || mt == DT_MAT_ALUMINUM || mt == DT_MAT_WATER ||
+               mt == DT_MAT_LINOLEUM;
+      b.glossy = (fs.mat[sid].flags & DT_F_GLOSSY) != 0;
       pts.clear();
       if (hd.type == DT_SHAPE_SPHERE) {
         const double r = std::sqrt(gp[dtd::SP_R2]);
@@ -408,7 +427,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
           bhi[a] = std::max(gp[dtd::CY_C1 + a], gp[dtd::CY_C2 + a]) + r;
         }
       } else if (shape_hull_points(hd, gp, 0.0, pts) && !pts.empty()) {
-        k = 0;
+        k = 2;
         for (int a = 0; a < 3; ++a) { blo[a] = INFINITY; bhi[a] = -INFINITY; }
         for (const P3& q : pts)
           for (int a = 0; a < 3; ++a) { blo[a] = std::min(blo[a], q[a]); bhi[a] = std::max(bhi[a], q[a]); }
@@ -423,13 +442,72 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       double sd = 0;
       for (int a = 0; a < 3; ++a) sd += (bhi[a] - blo[a]) * (bhi[a] - blo[a]);
       const double rho = 1e-6 * (1 + std::sqrt(sd));
-      for (int a = 0; a < 3; ++a) { blo[a] -= rho; bhi[a] += rho; }
-      // + 2e-3: the device picks the cell from o = p + 1e-3 sn, not from p
-      b.pad = eta_k[k] * diag + 2e-3;
+      // class 0: a rectangle or checkerboard whose box is flat in one axis has the exact axis
+      // normal (the cross product of two edges in that plane has two exact zeros), so X* lies on
+      // the box's plane; a near miss of the float checks only leaves the box within the plane
+      int flat = -1;
+      if (k == 2 && (hd.type == DT_SHAPE_RECTANGLE || hd.type == DT_SHAPE_CHECKERBOARD ||
+                     hd.type == DT_SHAPE_CHECKERBOARD_HOLE)) {
+        int nflat = 0;
+        for (int a = 0; a < 3; ++a)
+          if (bhi[a] == blo[a]) { flat = a; ++nflat; }
+        if (nflat == 1) k = 0;
+        else flat = -1;
+      }
+      for (int a = 0; a < 3; ++a)
+        if (a != flat) { blo[a] -= rho; bhi[a] += rho; }
+      b.pad = 0;
       b.k = k;
       sbox.push_back(b);
     }
     if (!bounded) occ.clear();
+    // The box of every ray origin (header): the camera's eye region and, around each shape whose
+    // material spawns secondary rays (refl_materials, cpp:574-576), where such a ray can start:
+    // isectP within eta |X* - start| of the shape's box, plus eps (1e-3) times the direction: the
+    // unit in / refl_ray (cpp:618, 765) or a glossy sample_refl (cpp:760), whose length stays below
+    // 1.5 |gloss_ray| + 7.2 <= 3080 (multiplier <= 2^11, the rectangle's length |lv| <= |gloss_ray|
+    // when lv falls back to the unnormalised cross product, the first rectangle's squeeze). Pass 1
+    // bounds |X* - start| by the root box's diagonal, pass 2 by the diagonal of pass 1's box and the
+    // shape's (starts lie in pass 1's box): each pass's box holds every origin by induction along the
+    // rays' parent chains.
+    auto box_diag = [](const double* alo, const double* ahi, const double* blo_, const double* bhi_) {
+      double s2 = 0;
+      for (int a = 0; a < 3; ++a) {
+        const double e = std::max(ahi[a], bhi_[a]) - std::min(alo[a], blo_[a]);
+        s2 += e * e;
+      }
+      return std::sqrt(s2) * (1 + 1e-9);
+    };
+    double blo1[3], bhi1[3];
+    for (int a = 0; a < 3; ++a) { blo1[a] = olo[a]; bhi1[a] = ohi[a]; }
+    if (!occ.empty()) {
+      for (int pass = 0; pass < 2; ++pass) {
+        double nlo[3], nhi[3];
+        for (int a = 0; a < 3; ++a) { nlo[a] = cam[a] - cam_r; nhi[a] = cam[a] + cam_r; }
+        for (const SBox& b : sbox) {
+          if (!b.refl) continue;
+          const double dist = pass == 0 ? diag + 1e-3 * 3080 * 2 : box_diag(blo1, bhi1, b.lo, b.hi);
+          const double pad = eta_k[b.k] * dist + 1e-3 * (b.glossy ? 3080.0 : 1.01) + 1e-9;
+          for (int a = 0; a < 3; ++a) {
+            nlo[a] = std::min(nlo[a], b.lo[a] - pad);
+            nhi[a] = std::max(nhi[a], b.hi[a] + pad);
+          }
+        }
+        // pass 1's box as it is (its pads may leave the root box); pass 2: both boxes hold every
+        // origin, so their intersection does
+        for (int a = 0; a < 3; ++a) {
+          blo1[a] = pass == 0 ? nlo[a] : std::max(nlo[a], blo1[a]);
+          bhi1[a] = pass == 0 ? nhi[a] : std::min(nhi[a], bhi1[a]);
+        }
+      }
+      // + 2e-3: the device picks the cell from o = p + 1e-3 sn, not from p
+      for (SBox& b : sbox) b.pad = eta_k[b.k] * box_diag(blo1, bhi1, b.lo, b.hi) + 2e-3;
+    }
+    g.org_check = true;
+    for (int a = 0; a < 3; ++a) { g.org_lo[a] = blo1[a]; g.org_hi[a] = bhi1[a]; }
+    if (timing)
+      fprintf(stderr, "dt: start-side origin box [%g %g %g] - [%g %g %g] (root and eye: [%g %g %g] - [%g %g %g])\n",
+              blo1[0], blo1[1], blo1[2], bhi1[0], bhi1[1], bhi1[2], olo[0], olo[1], olo[2], ohi[0], ohi[1], ohi[2]);
     auto occ_slab = [&](int z_lo, int z_hi) {
       for (const SBox& b : sbox) {
         int i0[3], i1[3];
@@ -455,7 +533,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
                 if (clo[a] > chi[a]) meet = false;
               }
               if (!meet) continue;
-              double* o = occ.data() + (((size_t)z * g.dim[1] + y) * g.dim[0] + x) * 12 + b.k * 6;
+              double* o = occ.data() + (((size_t)z * g.dim[1] + y) * g.dim[0] + x) * 6 * NK + b.k * 6;
               for (int a = 0; a < 3; ++a) { o[a] = std::min(o[a], clo[a]); o[3 + a] = std::max(o[3 + a], chi[a]); }
             }
       }
@@ -470,9 +548,9 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
       for (int z = 0; z < g.dim[2]; ++z)
         for (int y = 0; y < g.dim[1]; ++y)
           for (int x = 0; x < g.dim[0]; ++x) {
-            const double* o = occ.data() + (((size_t)z * g.dim[1] + y) * g.dim[0] + x) * 12;
-            double* q = bocc.data() + (((size_t)z * ob_ny + y / OB2) * ob_nx + x / OB) * 12;
-            for (int k = 0; k < 2; ++k)
+            const double* o = occ.data() + (((size_t)z * g.dim[1] + y) * g.dim[0] + x) * 6 * NK;
+            double* q = bocc.data() + (((size_t)z * ob_ny + y / OB2) * ob_nx + x / OB) * 6 * NK;
+            for (int k = 0; k < NK; ++k)
               for (int a = 0; a < 3; ++a) {
                 q[k * 6 + a] = std::min(q[k * 6 + a], o[k * 6 + a]);
                 q[k * 6 + 3 + a] = std::max(q[k * 6 + 3 + a], o[k * 6 + 3 + a]);
@@ -504,6 +582,14 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
         P.move = (ypad > 0 && hd.type == DT_SHAPE_RECTANGLE && (hd.flags & DT_F_NAMED_RECT))
                      ? std::fabs(P.n[1]) * ypad * (1 + 1e-9) + 1e-12 : 0.0;
         P.maxd = 1.02 * md + 1e-3 + P.move;
+        P.dblo = INFINITY;
+        P.dbhi = -INFINITY;
+        for (int q = 0; q < 8; ++q) {
+          double d = -P.c;
+          for (int a = 0; a < 3; ++a) d += P.n[a] * (((q >> a) & 1) ? g.org_hi[a] : g.org_lo[a]);
+          P.dblo = std::min(P.dblo, d);
+          P.dbhi = std::max(P.dbhi, d);
+        }
         s_plane[sid] = 1;
         int zeros = 0;
         for (int a = 0; a < 3; ++a) zeros += P.n[a] == 0.0;
@@ -533,7 +619,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
         return false;
     }
     const double* n = P.n;
-    const double c = P.c, maxd = P.maxd, mv = P.move;
+    const double c = P.c, mv = P.move;
     double lmax2 = 0, lmin2 = 0;
     for (int a = 0; a < 3; ++a) {
       const double far = std::max(std::fabs(chi[a] - llo[a]), std::fabs(lhi[a] - clo[a]));
@@ -546,23 +632,29 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
     // the range (a superset: the bound can only be lower)
     const bool one = c0[0] == c1[0] && c0[1] == c1[1] && c0[2] == c1[2];
     double mn = INFINITY;
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < NK; ++k) {
       double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
       auto take = [&](const double* o) {
         for (int a = 0; a < 3; ++a) { blo[a] = std::min(blo[a], o[a]); bhi[a] = std::max(bhi[a], o[3 + a]); }
       };
       if (one) {
-        take(occ.data() + (((size_t)c0[2] * g.dim[1] + c0[1]) * g.dim[0] + c0[0]) * 12 + k * 6);
+        take(occ.data() + (((size_t)c0[2] * g.dim[1] + c0[1]) * g.dim[0] + c0[0]) * 6 * NK + k * 6);
       } else {
         for (int z = c0[2]; z <= c1[2]; ++z)
           for (int by = c0[1] / OB2; by <= c1[1] / OB2; ++by)
             for (int bx = c0[0] / OB; bx <= c1[0] / OB; ++bx)
-              take(bocc.data() + (((size_t)z * ob_ny + by) * ob_nx + bx) * 12 + k * 6);
+              take(bocc.data() + (((size_t)z * ob_ny + by) * ob_nx + bx) * 6 * NK + k * 6);
       }
       if (!(blo[0] <= bhi[0] && blo[1] <= bhi[1] && blo[2] <= bhi[2])) continue;   // no such shape here
-      double d = -s * c;
-      for (int a = 0; a < 3; ++a) d += std::min(s * n[a] * blo[a], s * n[a] * bhi[a]);
-      mn = std::min(mn, d - mv - 2 * eta_k[k] * maxd);
+      double d = -s * c, ulo = -c, uhi = -c;
+      for (int a = 0; a < 3; ++a) {
+        d += std::min(s * n[a] * blo[a], s * n[a] * bhi[a]);
+        ulo += std::min(n[a] * blo[a], n[a] * bhi[a]);
+        uhi += std::max(n[a] * blo[a], n[a] * bhi[a]);
+      }
+      // |d(p) - d(X*)| <= eta |d(X*) - d(start)|: X* in these boxes, the start in the origin box
+      const double span = std::max(uhi, P.dbhi) - std::min(ulo, P.dblo);
+      mn = std::min(mn, d - mv - eta_k[k] * span * (1 + 1e-6) - 1e-12 * (1 + scale));
     }
     const double d_o = std::min(mn, 0.0) + 1e-3 * D / std::sqrt(lmax2);
     return d_o > 1e-7 * (1 + scale);
