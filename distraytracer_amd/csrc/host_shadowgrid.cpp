@@ -366,9 +366,12 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   const size_t nshape = fs.hdr.size();
   const int ncell_all = g.dim[0] * g.dim[1] * g.dim[2];
   // |t_f - t*| <= eta |t*| per class of closest-hit test (header): 0 axis-aligned plane tests, 1 the
-  // f32 quadratics, 2 every other planar test (tilted planes, triangles)
-  constexpr int NK = 3;
-  const double eta_k[NK] = {1.25e-7, 2e-3, 1e-6};
+  // f32 quadratics, 2 other planar tests (prism faces, triangles), 3 tilted rectangles and
+  // checkerboards (the culled shape's own points are bounded apart: occ3)
+  constexpr int NK = 4;
+  const double eta_k[NK] = {1.25e-7, 2e-3, 1e-6, 1e-6};
+  // per cell (occ3) and per aligned block (bocc3): the class-3 shape there, -1 none, -2 several
+  std::vector<int32_t> occ3, bocc3;
   std::vector<double> occ;                 // per cell and class: box (lo[3], hi[3]) of possible shading points
   std::vector<int8_t> s_plane;             // shapes tried as the culled one: 1 axis-aligned, 2 tilted (record in sp)
   // per shape tried as the culled one (start-side culling): plane, bounds and, per light, the side
@@ -376,6 +379,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
   struct SPlane {
     double n[3], c, maxd, move;
     double dblo, dbhi;         // n.x - c over the box of ray origins
+    double mvs[2];             // move toward the light box on side -1 / +1 (one-sided blur shifts)
     double sD[DT_MAX_SGRID];   // side * D per light (0: the light box is not on one side with margin)
     double box[6];             // tilted planes: the shape's own box (prefilter)
   };
@@ -401,7 +405,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
     for (size_t c = 0; c < bocc.size() / 6; ++c)
       for (int a = 0; a < 3; ++a) { bocc[c * 6 + a] = INFINITY; bocc[c * 6 + 3 + a] = -INFINITY; }
     // each shape's box (+ rho) and class, then the cells' boxes, on threads by z-slabs of cells
-    struct SBox { double lo[3], hi[3], pad; int k; bool refl, glossy; };
+    struct SBox { double lo[3], hi[3], pad; int k, sid; bool refl, glossy; };
     std::vector<SBox> sbox;
     bool bounded = true;
     std::vector<P3> pts;
@@ -452,12 +456,13 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
         for (int a = 0; a < 3; ++a)
           if (bhi[a] == blo[a]) { flat = a; ++nflat; }
         if (nflat == 1) k = 0;
-        else flat = -1;
+        else { flat = -1; k = 3; }
       }
       for (int a = 0; a < 3; ++a)
         if (a != flat) { blo[a] -= rho; bhi[a] += rho; }
       b.pad = 0;
       b.k = k;
+      b.sid = (int)sid;
       sbox.push_back(b);
     }
     if (!bounded) occ.clear();
@@ -500,6 +505,24 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
           bhi1[a] = pass == 0 ? nhi[a] : std::min(nhi[a], bhi1[a]);
         }
       }
+      // Cylinders: the box above holds the caps' centres +- r on every axis. X* lies on the
+      // infinite cylinder (or at the ray's closest approach, a near miss) within eta_1 |X* - start|
+      // of the slab between the caps, which p passed (cyl_in_caps), so on axis k it lies within
+      // r sqrt(1 - a_k^2) plus that of the caps' centres: C3's ceiling column no longer stretches
+      // 3 units above the ceiling
+      for (SBox& b : sbox) {
+        const dtd::DShapeHdr& hd = fs.hdr[b.sid];
+        if (hd.type != DT_SHAPE_CYLINDER && hd.type != DT_SHAPE_CHECKER_CYLINDER) continue;
+        const double* gp = fs.geom.data() + hd.off;
+        const double r = std::sqrt(gp[dtd::CY_R2]);
+        const double w = eta_k[1] * box_diag(blo1, bhi1, b.lo, b.hi) + 1e-6 * (1 + r);
+        for (int a = 0; a < 3; ++a) {
+          const double ax = gp[dtd::CY_AX + a];
+          const double e = r * std::sqrt(std::max(0.0, 1 - ax * ax)) * (1 + 1e-9) + w;
+          b.lo[a] = std::max(b.lo[a], std::min(gp[dtd::CY_C1 + a], gp[dtd::CY_C2 + a]) - e);
+          b.hi[a] = std::min(b.hi[a], std::max(gp[dtd::CY_C1 + a], gp[dtd::CY_C2 + a]) + e);
+        }
+      }
       // + 2e-3: the device picks the cell from o = p + 1e-3 sn, not from p
       for (SBox& b : sbox) b.pad = eta_k[b.k] * box_diag(blo1, bhi1, b.lo, b.hi) + 2e-3;
     }
@@ -533,12 +556,16 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
                 if (clo[a] > chi[a]) meet = false;
               }
               if (!meet) continue;
-              double* o = occ.data() + (((size_t)z * g.dim[1] + y) * g.dim[0] + x) * 6 * NK + b.k * 6;
+              const size_t ci_ = ((size_t)z * g.dim[1] + y) * g.dim[0] + x;
+              double* o = occ.data() + ci_ * 6 * NK + b.k * 6;
               for (int a = 0; a < 3; ++a) { o[a] = std::min(o[a], clo[a]); o[3 + a] = std::max(o[3 + a], chi[a]); }
+              if (b.k == 3) occ3[ci_] = occ3[ci_] == -1 || occ3[ci_] == b.sid ? b.sid : -2;
             }
       }
     };
     if (!occ.empty()) {
+      occ3.assign((size_t)ncell_all, -1);
+      bocc3.assign((size_t)ob_nx * ob_ny * g.dim[2], -1);
       const int nt = std::max(1, std::min({(int)std::thread::hardware_concurrency(), 16, g.dim[2]}));
       std::vector<std::thread> th;
       for (int t = 1; t < nt; ++t) th.emplace_back(occ_slab, g.dim[2] * t / nt, g.dim[2] * (t + 1) / nt);
@@ -555,6 +582,9 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
                 q[k * 6 + a] = std::min(q[k * 6 + a], o[k * 6 + a]);
                 q[k * 6 + 3 + a] = std::max(q[k * 6 + 3 + a], o[k * 6 + 3 + a]);
               }
+            const int32_t c3 = occ3[((size_t)z * g.dim[1] + y) * g.dim[0] + x];
+            int32_t& q3 = bocc3[((size_t)z * ob_ny + y / OB2) * ob_nx + x / OB];
+            if (c3 != -1) q3 = q3 == -1 || q3 == c3 ? c3 : -2;
           }
     }
     if (!occ.empty()) {
@@ -582,6 +612,11 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
         P.move = (ypad > 0 && hd.type == DT_SHAPE_RECTANGLE && (hd.flags & DT_F_NAMED_RECT))
                      ? std::fabs(P.n[1]) * ypad * (1 + 1e-9) + 1e-12 : 0.0;
         P.maxd = 1.02 * md + 1e-3 + P.move;
+        // with every shift >= 0 (up_only) the plane only moves by n_y v, v in [0, ypad]: toward
+        // the light box on side s (d = s (n.x - c)) by at most max(0, s n_y) ypad
+        for (int sd = 0; sd < 2; ++sd)
+          P.mvs[sd] = P.move == 0.0 || !up_only ? P.move
+                                                : std::max(0.0, (sd ? 1.0 : -1.0) * P.n[1]) * ypad * (1 + 1e-9) + 1e-12;
         P.dblo = INFINITY;
         P.dbhi = -INFINITY;
         for (int q = 0; q < 8; ++q) {
@@ -611,15 +646,30 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
     const double sD = P.sD[l];
     if (sD == 0) return false;
     const double s = sD > 0 ? 1.0 : -1.0, D = std::fabs(sD);
-    // a tilted plane whose own box meets the cells: the box's corners leave the plane by far more
-    // than the margin, so the bound fails (a host-time prefilter; it only keeps leaves)
-    if (s_plane[sid] == 2) {
+    const bool one = c0[0] == c1[0] && c0[1] == c1[1] && c0[2] == c1[2];
+    // the class-3 shape of the cells (-1 none, -2 several): when it is the culled shape itself, its
+    // points are bounded by its own plane test (below), not by their box
+    int32_t id3 = -1;
+    if (one) {
+      id3 = occ3[((size_t)c0[2] * g.dim[1] + c0[1]) * g.dim[0] + c0[0]];
+    } else {
+      for (int z = c0[2]; z <= c1[2]; ++z)
+        for (int by = c0[1] / OB2; by <= c1[1] / OB2; ++by)
+          for (int bx = c0[0] / OB; bx <= c1[0] / OB; ++bx) {
+            const int32_t q3 = bocc3[((size_t)z * ob_ny + by) * ob_nx + bx];
+            if (q3 != -1) id3 = id3 == -1 || id3 == q3 ? q3 : -2;
+          }
+    }
+    // a tilted plane whose own box meets the cells along with other tilted planes: the box's
+    // corners leave the plane by far more than the margin, so the bound fails (a host-time
+    // prefilter; it only keeps leaves)
+    if (s_plane[sid] == 2 && id3 != sid) {
       const double* b = P.box;
       if (b[0] <= chi[0] && b[3] >= clo[0] && b[1] <= chi[1] && b[4] >= clo[1] && b[2] <= chi[2] && b[5] >= clo[2])
         return false;
     }
     const double* n = P.n;
-    const double c = P.c, mv = P.move;
+    const double c = P.c, mv = P.mvs[sD > 0 ? 1 : 0];
     double lmax2 = 0, lmin2 = 0;
     for (int a = 0; a < 3; ++a) {
       const double far = std::max(std::fabs(chi[a] - llo[a]), std::fabs(lhi[a] - clo[a]));
@@ -630,9 +680,17 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
     if (!(lmin2 > 4e-6)) return false;
     // the cells' boxes of possible shading points: the cell's own, or the aligned blocks covering
     // the range (a superset: the bound can only be lower)
-    const bool one = c0[0] == c1[0] && c0[1] == c1[1] && c0[2] == c1[2];
     double mn = INFINITY;
     for (int k = 0; k < NK; ++k) {
+      if (k == 3 && id3 == sid) {
+        // the culled shape's own points (header): its plane test puts p within
+        // 1.25e-7 |d(start)| + O(2^-53 size) of its own plane. A moving rectangle is tested in the
+        // pass's shifted scene, the shading points' and the culled plane alike: the bound holds for
+        // the shifted plane, whose distances from the origins grow by at most mv (D already less mv)
+        const double dmax = std::max(std::fabs(P.dblo), std::fabs(P.dbhi)) + P.move;
+        mn = std::min(mn, -1.25e-7 * dmax * (1 + 1e-6) - 1e-12 * (1 + scale));
+        continue;
+      }
       double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
       auto take = [&](const double* o) {
         for (int a = 0; a < 3; ++a) { blo[a] = std::min(blo[a], o[a]); bhi[a] = std::max(bhi[a], o[3 + a]); }
@@ -853,7 +911,7 @@ bool build_shadow_grid(const std::vector<dtd::DNodeDev>& nodes, const FlatScene&
           dhi = std::max(dhi, d);
         }
         const int side = dlo > 0 ? 1 : dhi < 0 ? -1 : 0;
-        const double D = (side > 0 ? dlo : -dhi) - P.move;
+        const double D = (side > 0 ? dlo : -dhi) - (side > 0 ? P.mvs[1] : P.mvs[0]);
         // the far end's margin (header): D - 1e-3 above 1e-5 maxdist
         if (side != 0 && D - 1e-3 > 1e-5 * P.maxd) P.sD[l] = side * D;
       }
