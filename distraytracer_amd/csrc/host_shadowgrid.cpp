@@ -97,8 +97,20 @@
 // maxdist (|d| over the root box and the eye region), and the cell box keeps 2e-3 from the light
 // box. The origin box is recorded: a render whose camera's eye region leaves it walks the trees
 // (dt_api.cpp prepare_render). host_accel.cpp builds the lists with it only where they fit
-// (DT_SG_START). Only axis-aligned planes profit (a tilted shape's box is not flat), and only
-// rectangles and checkerboards are tried as the culled shape.
+// (DT_SG_START). Only rectangles and checkerboards are tried as the culled shape.
+// A tilted rectangle or checkerboard (class 3; C3's ceiling sinks by 0.025 across the room) has a
+// box that leaves its plane, so the box bound fails in the cells that hold it. Its own points are
+// bounded by its own plane test instead: with num = (A - start).n and dn = (float)(ray.n),
+// d(p) = d(start) + dn t_f = d(start) (r - e) + e_num (1 - r)(1 + e), |e| <= 2.0001 * 2^-24, where
+// r = e_dn / (dn + e_dn) carries the f64 dot product's error e_dn <= 2^-53 sqrt(3) |ray| and
+// |d(start) r| ~ t_f |e_dn| <= 2^-53 sqrt(3) |p - start|: so |d(p)| <= 1.25e-7 |d(start)| +
+// 1e-12 (1 + scale) whatever the angle. Per cell and aligned block the host keeps which class-3
+// shape is there (none, one, several); where it is the culled shape alone, its points take that
+// bound and the box bound serves the other classes. Cylinders' boxes are the axis segment's
+// widened by r sqrt(1 - a_k^2) per axis plus eta_1 times the origin box's diagonal (X* lies that
+// close to the slab between the caps that p passed), not the caps' centres +- r on every axis.
+// Blur shifts that are all >= 0 (up_only) move a "rectangle"'s plane toward the light box on side
+// s by at most max(0, s n_y) ypad, not |n_y| ypad.
 // With ypad > 0 (blur passes) every "rectangle" moves by up to ypad in y: its box grows by ypad in
 // y, and as the culled shape its plane moves by |n_y| ypad (nothing for a wall with a horizontal
 // normal), which D and the bound lose. C3: the ceiling, back and side walls leave the lists of the
