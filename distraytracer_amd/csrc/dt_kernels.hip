@@ -1981,18 +1981,21 @@ __device__ bool occluded_union(const DScene& S, const Walk& w, bool active, V3 b
     if (m == INT_MAX) break;
     const DNodeDev nd = cas(S.nodes)[m];
     const bool live = inv(am & ~om);
+    // only the lanes whose own list holds leaf m test it: m cannot occlude the others (their lists
+    // hold every leaf that can), and a wave whose listing lanes all miss m's box skips its shapes
+    const bool has = head == m;
     DT_WK(DT_WK_BOX, live);
     DT_WK(DT_WK_BOX, BUMP && live);
     DT_CNT(34);
     if (BUMP && SF) {
-      const unsigned long long cand = __ballot(live && bump_box(S, w, m, shift, bstart));
+      const unsigned long long cand = __ballot(live && has && bump_box(S, w, m, shift, bstart));
       if (cand) shadow_leaf_bump(S, nd, m, w, cand, om, bstart, sn, sstart, t_max, skip_shape, shift, cnt);
     } else {
-      const unsigned long long hbm = BUMP ? __ballot(live & bump_leaf_gathered(S, w, m, shift, bstart))
-                                          : (am & ~om) & box_mask_finite(nd, w.rb, bstart, tcull);
+      const unsigned long long hbm = BUMP ? __ballot(live & has & bump_leaf_gathered(S, w, m, shift, bstart))
+                                          : (am & ~om) & __ballot(has) & box_mask_finite(nd, w.rb, bstart, tcull);
       if (hbm) shadow_leaf(S, nd, hbm, om, sn, sstart, t_max, skip_shape, shift, cnt);
     }
-    if (head == m) {
+    if (has) {
       ++k;
       head = nxt;
       nxt = k + 1 < n ? S.sg_list[off + k + 1] : INT_MAX;
