@@ -1465,6 +1465,9 @@ static_assert(DT_SHAPE_CHECKERBOARD == 6 && DT_SHAPE_CHECKERBOARD_HOLE == 7 && D
               "DT_HAS(6/7/8) below");
 // scattered shadow waves: lanes whose own cell is an umbra cell answer "occluded" without joining
 // the union of the lanes' lists (the coherent path already answered a whole wave so)
+#ifndef DT_UMBRA_EARLY
+#define DT_UMBRA_EARLY 1   // umbra cells of point lights decided before the light sample (light loop)
+#endif
 #ifndef DT_UMBRA_LANES
 #define DT_UMBRA_LANES 1
 #endif
@@ -2962,19 +2965,39 @@ __device__ __forceinline__ void run_pass(const Ctx& c_in, bool active, V3 ray0, 
         V3 sray = v3(1, 0, 0);
         float t_max = 0;
         V3 sn = v3(1, 0, 0);
-        if (walk) {
+        // A point light (no draw) whose umbra holds the shading point's own grid cell: the shadow
+        // ray starts at o = p + 1e-3 sn, inside the cell's box widened by m1 >= 0.05 cells, over
+        // which the umbra is proven (host_shadowgrid.cpp), so it is occluded before the sample,
+        // the ray setup and the walk. Unshifted lanes only (pass-0 geometry). C3's window light.
+        bool umb0 = false;
+        if (DT_UMBRA_EARLY && L.type == DT_LIGHT_POINT && li < P.sg_n && P.sg_base0[li] >= 0 && walk &&
+            shift == 0.0f) {
+          float x, y, z;
+          sg_coords(P, isectP, x, y, z);
+          const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
+          if (fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.sg_dim[0] && fy < (float)P.sg_dim[1] &&
+              fz < (float)P.sg_dim[2]) {
+            const int cl = ((int)fz * P.sg_dim[1] + (int)fy) * P.sg_dim[0] + (int)fx;
+            umb0 = (((const uint2*)S.sg_cells)[(size_t)P.sg_base0[li] + cl].x & DT_SG_UMBRA) != 0u;
+          }
+        }
+        const bool ws = walk && !umb0;
+        if (ws) {
           DT_WK(DT_WK_LIGHT, true);
           sray = light_sample(c, L, li, isectP, node, cnt.wc + WC_SPHL, pair);
           t_max = (float)norm(sray);
           sn = normalized(sray);
-          DT_WCNT(WC_SHADOW, true);
         }
+        DT_WCNT(WC_SHADOW, walk);
         DT_T(t4);
 #ifdef DT_STAMPS
         cnt.cur_li = li;
 #endif
-        bool occl = occluded(S, P, walk, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)),
-                             t_max, L.shape_index, li, shift, cnt);
+        bool occl = umb0;
+        if (!DT_UMBRA_EARLY || __ballot(ws))
+          occl = occluded(S, P, ws, sray, add(isectP, mul(1e-3, sray)), sn, add(isectP, mul(1e-3, sn)), t_max,
+                          L.shape_index, li, shift, cnt) ||
+                 umb0;
         DT_T(t5);
         DT_ACC(3, t4, t5);
 #ifdef DT_STAMPS
