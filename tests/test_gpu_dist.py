@@ -50,7 +50,10 @@ def _globals(spp=16, W=400, H=300):
 def _rank(rank, world, port, outdir):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a file rendezvous in the test's own directory: a TCP store on a port probed free beforehand
+    # can lose it to another process (EADDRINUSE seen on a GPU box)
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(outdir, "rdv"), rank=rank,
+                            world_size=world)
     try:
         from distraytracer_amd.multigpu import FrameSplit, GatherPipeline
         torch.cuda.set_device(0)
@@ -139,7 +142,10 @@ def _rank_device_path(rank, world, port, outdir, shape=(16, 400, 300)):
     stream into device slabs, GatherPipeline.begin / submit / finish, the device scatter on rank 0)."""
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a file rendezvous in the test's own directory: a TCP store on a port probed free beforehand
+    # can lose it to another process (EADDRINUSE seen on a GPU box)
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(outdir, "rdv"), rank=rank,
+                            world_size=world)
     try:
         from distraytracer_amd.multigpu import FrameSplit, GatherPipeline
         torch.cuda.set_device(0)
