@@ -9,7 +9,6 @@ on the GPU, against the CPU oracle:
     bump tree's one-sided padding assumed fall back to exact walks.
 """
 import os
-import socket
 import subprocess
 
 import numpy as np
@@ -62,22 +61,15 @@ def test_dtrender_cli_matches_oracle(cuda, tmp_path, mode, args, builder, frame,
     log_equal("dtrender %s PPM bytes vs writePPM(oracle)" % mode, px, ref_px)
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def test_gather_pipeline_over_rccl(cuda):
+def test_gather_pipeline_over_rccl(cuda, tmp_path):
     """bench.py's N > 1 path at world size 1 over the real NCCL (= RCCL) backend: frames render
     into double-buffered slabs on torch's stream, GatherPipeline gathers them asynchronously and
     scatters on rank 0 with dt_unpack_slabs on the same stream. The assembled image equals a plain
     full-frame render of the same frame, for every frame of the pipeline."""
     import torch.distributed as dist
     from distraytracer_amd.multigpu import FrameSplit, GatherPipeline
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1,
+    # a file rendezvous (a port probed free beforehand can be lost to another process)
+    dist.init_process_group("nccl", init_method="file://" + str(tmp_path / "rdv"), rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     try:
         g = dt.globals_default()
@@ -111,14 +103,15 @@ def test_gather_pipeline_over_rccl(cuda):
         dist.destroy_process_group()
 
 
-def test_gather_pipeline_two_streams_over_rccl(cuda):
+def test_gather_pipeline_two_streams_over_rccl(cuda, tmp_path):
     """bench.py's N > 1 path with two frames in flight (its default): frame k renders on
     streams[k % 2] with a scene object of its own, GatherPipeline orders the gather after the render
     by an event and the next render into a slab after that slab's gather. Every assembled image
     equals a plain full-frame render of its frame."""
     import torch.distributed as dist
     from distraytracer_amd.multigpu import FrameSplit, GatherPipeline
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1,
+    # a file rendezvous (a port probed free beforehand can be lost to another process)
+    dist.init_process_group("nccl", init_method="file://" + str(tmp_path / "rdv"), rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     try:
         g = dt.globals_default()
